@@ -1,0 +1,244 @@
+"""Benchmark of the stereo hot path (BASELINE.json metric) on 1..N MI355X GPUs.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one pass of the hot path over one batch of synthetic rectified pairs already resident
+in HBM: StereoSGBM::compute (prefilter, BT cost, block sum, path aggregation, WTA/uniqueness/
+subpixel, LR check, median 3x3, speckle filter) + convertTo(1/16) + reprojectImageTo3D.
+Frames shard across ranks (rank r owns its own frame stream); with N > 1 each step's int16
+disparity is gathered to rank 0 over RCCL (the north star's frame-shard + gather).  Rank 0
+prints one JSON line.  value = all ranks' pixels / max-over-ranks wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "stereo Mpix/s (disparity+reproject) at 1280×720 d=128, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+# name -> (description, W, H, SGBM args (create order), batch, reproject handleMissing)
+CONFIGS = {
+    "c2": ("C2 (BASELINE configs[1]): 1280x720 d=128 MODE_SGBM 5-path + reprojectImageTo3D(Q, "
+           "handleMissing), batch 1", 1280, 720, (0, 128, 5, 600, 2400, 1, 63, 12, 200, 2, 0), 1, True),
+    "c3": ("C3 (configs[2]): 1280x720 d=256 MODE_HH 8-path + reproject, batch 32", 1280, 720,
+           (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, 1), 32, True),
+    "c0": ("C0 reference-exact matcher: 640x360 d=80 MODE_SGBM_3WAY (stereo_disparity.cpp:5-9) + reproject",
+           640, 360, (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, False),
+    "pcd": ("pcd_write.cpp:102-116: 1280x720 d=80 MODE_SGBM_3WAY + reproject(handleMissing)", 1280, 720,
+            (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, True),
+}
+MODE_NAMES = {0: "MODE_SGBM", 1: "MODE_HH", 2: "MODE_SGBM_3WAY"}
+NPATHS = {0: 5, 1: 8, 2: 3}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg, seconds_target=15.0):
+    """The oracle (C restatement of OpenCV 4.6 SGBM + reprojectImageTo3D) timed on host cores,
+    one frame per thread (ctypes releases the GIL), on a bounded sample."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+    from stereo_depth_ruler_amd import synthetic as S
+
+    _, W, H, args, _, hm = cfg
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    L, R, _ = S.make_pair(H, W, args[1], seed=12345)
+    p = O.make_params(*args)
+
+    def one(_):
+        d = O.sgbm_compute(L, R, p)
+        O.reproject(O.disp_to_float(d), S.REFERENCE_Q, hm)
+        return 1
+
+    frames = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds_target:
+            frames += sum(ex.map(one, range(threads)))
+    el = time.perf_counter() - t0
+    return {
+        "value": round(frames * W * H / el / 1e6, 4),
+        "unit": "Mpix/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{frames} frames of {W}x{H} d={args[1]} {MODE_NAMES[args[10]]} full compute (median+speckle) "
+                  f"+ reproject, {threads} threads x 1 frame each, {el:.1f} s wall; oracle/sgbm_oracle.c "
+                  f"(C restatement of OpenCV 4.6 StereoSGBM; OpenCV itself is absent on this image)",
+    }
+
+
+def load_traffic(kernel_tag):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel_tag, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import stereo_depth_ruler_amd as sdr
+    from stereo_depth_ruler_amd import synthetic as S
+    from stereo_depth_ruler_amd.sgbm import KERNEL_PATH_ADD
+
+    desc, W, H, args, batch, hm = CONFIGS[a.config]
+    D, mode = args[1], args[10]
+    nf = max(a.frames, batch)
+    Ls, Rs = S.make_batch(nf, H, W, D, seed0=1000 * rank)
+    Ld = torch.from_numpy(Ls).to(dev)
+    Rd = torch.from_numpy(Rs).to(dev)
+    m = sdr.StereoSGBM.create(*args, device=dev.index)
+    disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
+    xyz = torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev)
+    gather_bufs = None
+    if world > 1 and rank == 0:
+        gather_bufs = [[torch.empty_like(disp[0]) for _ in range(world)] for _ in range(2)]
+    pending = [None, None]
+
+    def step(i):
+        j = (i * batch) % (nf - batch + 1) if nf > batch else 0
+        slot = i & 1
+        if pending[slot] is not None:
+            pending[slot].wait()
+            pending[slot] = None
+        m.compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot], xyz=xyz)
+        if world > 1:
+            pending[slot] = dist.gather(disp[slot], gather_bufs[slot] if rank == 0 else None, dst=0,
+                                        async_op=True)
+
+    for i in range(a.warmup):
+        step(i)
+    for p in pending:
+        if p is not None:
+            p.wait()
+    pending = [None, None]
+    torch.cuda.synchronize()
+    if not a.no_kernel_timing:
+        m.enable_timing(2)
+        m.kernel_time(-1, reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i)
+    for p in pending:
+        if p is not None:
+            p.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    roofline = None
+    if not a.no_kernel_timing:
+        tot_ms, cnt = m.kernel_time(KERNEL_PATH_ADD, reset=False)
+        all_ms, all_cnt = m.kernel_time(-1, reset=True)
+        m.enable_timing(0)
+        w1 = W - max(args[0] + D, 0) + min(args[0], 0)
+        cells = batch * H * w1 * D
+        bytes_per_launch = cells * 6  # C read (2 B) + S read (2 B) + S write (2 B) per cell
+        if cnt:
+            avg_s = tot_ms / cnt / 1e3
+            achieved = bytes_per_launch / avg_s / 1e9
+            roofline = {
+                "bound": "hbm",
+                "kernel": "k_path<DPL=2,S_ADD> (middle path directions, 3 launches/frame)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic("k_path_add"),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "avg_launch_us": round(avg_s * 1e6, 2),
+                "launches_timed": cnt,
+                "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
+            }
+
+    pix = world * a.steps * batch * W * H
+    value = pix / el / 1e6
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic seeded rectified pairs (SURVEY.md 8d recipe); reference assets absent",
+        "config": {
+            "workload": desc,
+            "width": W, "height": H, "numDisparities": D, "mode": MODE_NAMES[mode],
+            "paths": NPATHS[mode], "batch": batch,
+            "params": dict(zip(["minDisparity", "numDisparities", "blockSize", "P1", "P2",
+                                "disp12MaxDiff", "preFilterCap", "uniquenessRatio",
+                                "speckleWindowSize", "speckleRange", "mode"], args)),
+            "parallelism": f"frame shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+        },
+        "fps": round(world * a.steps * batch / el, 2),
+        "roofline": roofline,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(CONFIGS[a.config])
+        except Exception as e:  # the baseline never hides the GPU number
+            log("cpu baseline failed:", repr(e))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    m.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * sdr.h -- C ABI of the MI355X-native stereo disparity engine (stereo_depth_ruler_amd).
+ *
+ * Drop-in boundary for the reference's hot path: every entry point takes plain pointers and
+ * sizes (no OpenCV, no torch types) and replaces one OpenCV call the reference makes:
+ *
+ *   sdr_sgbm_create / sdr_sgbm_set_params
+ *       <- cv::StereoSGBM::create(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, MODE_SGBM_3WAY)
+ *          stereo_vision/src/stereo_disparity.cpp:5-9, point_cloud/src/pcd_write.cpp:102-108
+ *   sdr_sgbm_compute / sdr_sgbm_compute_device
+ *       <- matcher->compute(L, R, disp)  stereo_vision/src/stereo_disparity.cpp:27-28,
+ *          sgbm->compute(left_gray, right_gray, disp)  point_cloud/src/pcd_write.cpp:111
+ *   sdr_reproject / sdr_reproject_device / sdr_disp16_reproject_device
+ *       <- cv::reprojectImageTo3D(disp, xyz, Q, handleMissing)  stereo_disparity.cpp:78,
+ *          pcd_write.cpp:116 (with disp.convertTo(CV_32F, 1/16) at pcd_write.cpp:112)
+ *   sdr_bgr2gray_device / sdr_resize_area_half_device
+ *       <- cv::cvtColor(BGR2GRAY) / cv::resize(0.5, INTER_AREA)  stereo_disparity.cpp:19-24
+ *   sdr_right_matcher_params
+ *       <- cv::ximgproc::createRightMatcher(matcher)  stereo_disparity.cpp:10
+ *
+ * Error behaviour mirrors the CV_Assert()s of StereoSGBMImpl::compute: a negative status is
+ * returned instead of throwing; sdr_last_error() returns the thread's last message.
+ * Threading: one handle = one HIP stream + scratch; a handle must not be used by two threads at
+ * once (as with cv::StereoSGBM, whose impl owns a scratch buffer); handles are independent.
+ */
+#ifndef SDR_SDR_H
+#define SDR_SDR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDR_ABI_VERSION 1
+
+/* cv::StereoSGBM::MODE_* */
+enum { SDR_MODE_SGBM = 0, SDR_MODE_HH = 1, SDR_MODE_SGBM_3WAY = 2, SDR_MODE_HH4 = 3 };
+
+/* uniqueness test form: AUTO = 3WAY uses OpenCV's SIMD threshold form
+ * cost <= (100*minS)/(100-u), SGBM/HH the scalar form cost*(100-u) < minS*100 */
+enum { SDR_UNIQ_AUTO = 0, SDR_UNIQ_SCALAR = 1, SDR_UNIQ_SIMD = 2 };
+
+/* status codes */
+enum {
+    SDR_OK = 0,
+    SDR_ERR_ARG = -1,         /* null pointer, non-positive size, bad stride */
+    SDR_ERR_NUMDISP = -2,     /* numDisparities <= 0 or not a multiple of 16 (OpenCV assert) */
+    SDR_ERR_MODE = -3,        /* unsupported mode (MODE_HH4) */
+    SDR_ERR_SIZE = -4,        /* image too narrow for the disparity range / block size */
+    SDR_ERR_TYPE = -5,        /* channels != 1 (8-bit single channel, as the reference passes) */
+    SDR_ERR_DEVICE = -6,      /* HIP runtime error */
+    SDR_ERR_NOMEM = -7,
+    SDR_ERR_LIMIT = -8        /* numDisparities > 256 (engine limit) */
+};
+
+/* Field order and meaning of cv::StereoSGBM::create(...) + two knobs OpenCV fixes internally. */
+typedef struct sdr_sgbm_params {
+    int minDisparity;
+    int numDisparities;
+    int blockSize;
+    int P1;
+    int P2;
+    int disp12MaxDiff;
+    int preFilterCap;
+    int uniquenessRatio;
+    int speckleWindowSize;
+    int speckleRange;
+    int mode;
+    int nstripes;   /* MODE_SGBM_3WAY stripes; 0 -> 4 (OpenCV 4.x fixed value) */
+    int uniq_rule;  /* SDR_UNIQ_* */
+} sdr_sgbm_params;
+
+typedef struct sdr_sgbm sdr_sgbm;
+
+/* StereoSGBM::create defaults: (0, 16, 3, 0, 0, 0, 0, 0, 0, 0, MODE_SGBM) */
+void sdr_sgbm_params_default(sdr_sgbm_params* p);
+/* createRightMatcher: minD' = -(minD+numD)+1, uniqueness 0, disp12MaxDiff 1e6, speckle off */
+void sdr_right_matcher_params(const sdr_sgbm_params* left, sdr_sgbm_params* right);
+
+int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out);
+int sdr_sgbm_destroy(sdr_sgbm* h);
+int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p);
+int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p);
+/* HIP stream (hipStream_t) the handle launches on; 0 = the handle's own stream. */
+int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
+void* sdr_sgbm_get_stream(const sdr_sgbm* h);
+
+/* Host-pointer compute (H2D, compute, D2H, synchronous): left/right 8-bit, `stride` bytes per
+ * row; disp int16 (1/16 px), `disp_stride` ELEMENTS per row. */
+int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int width, int height,
+                     int channels, size_t stride, int16_t* disp, size_t disp_stride);
+
+/* Device-pointer batch compute, asynchronous on the handle's stream: nframes frames spaced
+ * frame_stride bytes (inputs) / disp_frame_stride elements (output) apart. */
+int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* d_left, const uint8_t* d_right,
+                            int width, int height, size_t stride, size_t frame_stride,
+                            int nframes, int16_t* d_disp, size_t disp_stride,
+                            size_t disp_frame_stride);
+
+/* Fused hot path of point_cloud/src/pcd_write.cpp:111-116 on device: compute + convertTo(1/16)
+ * + reprojectImageTo3D(Q, handle_missing) -> xyz float32x3 [nframes][height][width][3]. */
+int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* d_left, const uint8_t* d_right,
+                                      int width, int height, size_t stride, size_t frame_stride,
+                                      int nframes, int16_t* d_disp, const double Q[16],
+                                      int handle_missing, float* d_xyz);
+
+/* reprojectImageTo3D on a CV_32F disparity (host pointers, synchronous). */
+int sdr_reproject(const float* disp, int width, int height, size_t disp_stride, const double Q[16],
+                  int handle_missing, float* xyz, size_t xyz_stride);
+/* Device versions (asynchronous on `stream`, a hipStream_t; NULL = default stream). */
+int sdr_reproject_device(const float* d_disp, int width, int height, size_t disp_stride,
+                         const double Q[16], int handle_missing, float* d_xyz, size_t xyz_stride,
+                         int nframes, void* stream);
+int sdr_disp16_reproject_device(const int16_t* d_disp, int width, int height, size_t disp_stride,
+                                const double Q[16], int handle_missing, float* d_xyz,
+                                size_t xyz_stride, int nframes, void* stream);
+/* disp.convertTo(f, CV_32F, 1/16) on device. */
+int sdr_disp16_to_float_device(const int16_t* d_disp, float* d_out, size_t n, void* stream);
+
+/* Class-path pre-steps on device (stereo_disparity.cpp:19-24). */
+int sdr_bgr2gray_device(const uint8_t* d_bgr, int width, int height, size_t bgr_stride,
+                        uint8_t* d_gray, size_t gray_stride, int nframes, void* stream);
+int sdr_resize_area_half_device(const uint8_t* d_src, int width, int height, size_t stride,
+                                uint8_t* d_dst, size_t dst_stride, int nframes, void* stream);
+
+/* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
+size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);
+
+/* Timing with HIP events on the handle's stream.  level 1: per-stage timing of the last compute
+ * (sdr_sgbm_last_timing: cost volume / path aggregation / LR+median+speckle, ms).  level 2 also
+ * brackets every kernel launch; sdr_sgbm_kernel_time sums the launches of one SDR_KERNEL_* kind
+ * (kind < 0: all) since the last reset. */
+enum {
+    SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATH_WRITE = 2,
+    SDR_KERNEL_PATH_ADD = 3, SDR_KERNEL_PATH_WTA = 4, SDR_KERNEL_LR = 5, SDR_KERNEL_MEDIAN = 6,
+    SDR_KERNEL_SPECKLE = 7, SDR_KERNEL_REPROJECT = 8
+};
+int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
+int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);
+int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int* count);
+
+/* Device self-test of the cross-lane primitives the kernels rely on (DPP wave shifts,
+ * permlane swaps); fills 4 failure counters, all zero on a healthy gfx950. */
+int sdr_selftest_wave_ops(int* failures4);
+
+/* Diagnostics: synchronously copy an internal buffer of the last compute to host memory.
+ * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,
+ * 2 = after the LR check, 3 = final (median + speckle), 4 = wta keys [F][H][W1] u32. */
+int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
+
+const char* sdr_last_error(void);
+int sdr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

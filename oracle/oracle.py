@@ -1,0 +1,162 @@
+"""ctypes loader for the CPU restatement (oracle/sgbm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker / CPU baseline.  The product (stereo_depth_ruler_amd) never imports it.
+Parity against real OpenCV 4.6.0 is UNPINNED (see sgbm_oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+MODE_SGBM, MODE_HH, MODE_SGBM_3WAY = 0, 1, 2
+UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
+STAGE_MEDIAN, STAGE_SPECKLE = 1, 2
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "minDisparity", "numDisparities", "blockSize", "P1", "P2", "disp12MaxDiff",
+        "preFilterCap", "uniquenessRatio", "speckleWindowSize", "speckleRange", "mode",
+        "nstripes", "uniq_rule")]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        i16p = ctypes.POINTER(ctypes.c_int16)
+        f32p = ctypes.POINTER(ctypes.c_float)
+        f64p = ctypes.POINTER(ctypes.c_double)
+        sz = ctypes.c_size_t
+        ci = ctypes.c_int
+        L.orc_sgbm_compute_stages.argtypes = [u8p, u8p, ci, ci, sz, ctypes.POINTER(OrcParams), i16p, sz, ci]
+        L.orc_sgbm_compute_stages.restype = ci
+        L.orc_cost_volume.argtypes = [u8p, u8p, ci, ci, sz, ctypes.POINTER(OrcParams), i16p]
+        L.orc_cost_volume.restype = ci
+        L.orc_pixel_cost_row.argtypes = [u8p, u8p, ci, ci, sz, ci, ci, ci, ci, i16p]
+        L.orc_pixel_cost_row.restype = ci
+        L.orc_median3x3_s16.argtypes = [i16p, i16p, ci, ci]
+        L.orc_filter_speckles_s16.argtypes = [i16p, ci, ci, ci, ci, ci]
+        L.orc_reproject_f32.argtypes = [f32p, ci, ci, f64p, ci, f32p]
+        L.orc_bgr2gray.argtypes = [u8p, ci, ci, sz, u8p]
+        L.orc_resize_area_half.argtypes = [u8p, ci, ci, sz, u8p]
+        L.orc_disp_to_float.argtypes = [i16p, ci, f32p]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def make_params(minDisparity=0, numDisparities=16, blockSize=3, P1=0, P2=0, disp12MaxDiff=0,
+                preFilterCap=0, uniquenessRatio=0, speckleWindowSize=0, speckleRange=0,
+                mode=MODE_SGBM, nstripes=4, uniq_rule=UNIQ_AUTO) -> OrcParams:
+    """Argument order and defaults of cv::StereoSGBM::create."""
+    return OrcParams(minDisparity, numDisparities, blockSize, P1, P2, disp12MaxDiff, preFilterCap,
+                     uniquenessRatio, speckleWindowSize, speckleRange, mode, nstripes, uniq_rule)
+
+
+def sgbm_compute(left: np.ndarray, right: np.ndarray, params: OrcParams,
+                 stages: int = STAGE_MEDIAN | STAGE_SPECKLE) -> np.ndarray:
+    left = np.ascontiguousarray(left, dtype=np.uint8)
+    right = np.ascontiguousarray(right, dtype=np.uint8)
+    assert left.shape == right.shape and left.ndim == 2
+    h, w = left.shape
+    out = np.empty((h, w), np.int16)
+    rc = lib().orc_sgbm_compute_stages(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w,
+                                       ctypes.byref(params), _p(out, ctypes.c_int16), w, stages)
+    if rc != 0:
+        raise ValueError(f"orc_sgbm_compute failed: {rc}")
+    return out
+
+
+def cost_volume(left, right, params: OrcParams) -> np.ndarray:
+    left = np.ascontiguousarray(left, dtype=np.uint8)
+    right = np.ascontiguousarray(right, dtype=np.uint8)
+    h, w = left.shape
+    minD, D = params.minDisparity, params.numDisparities
+    w1 = (w + min(minD, 0)) - max(minD + D, 0)
+    out = np.empty((h, w1, D), np.int16)
+    rc = lib().orc_cost_volume(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w,
+                               ctypes.byref(params), _p(out, ctypes.c_int16))
+    if rc != 0:
+        raise ValueError(f"orc_cost_volume failed: {rc}")
+    return out
+
+
+def pixel_cost_row(left, right, y, minD, numD, preFilterCap) -> np.ndarray:
+    left = np.ascontiguousarray(left, dtype=np.uint8)
+    right = np.ascontiguousarray(right, dtype=np.uint8)
+    h, w = left.shape
+    w1 = (w + min(minD, 0)) - max(minD + numD, 0)
+    out = np.empty((w1, numD), np.int16)
+    rc = lib().orc_pixel_cost_row(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w, y,
+                                  minD, numD, preFilterCap, _p(out, ctypes.c_int16))
+    if rc != 0:
+        raise ValueError(f"orc_pixel_cost_row failed: {rc}")
+    return out
+
+
+def median3x3(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.int16)
+    h, w = src.shape
+    dst = np.empty_like(src)
+    lib().orc_median3x3_s16(_p(src, ctypes.c_int16), _p(dst, ctypes.c_int16), w, h)
+    return dst
+
+
+def filter_speckles(img: np.ndarray, new_val: int, max_size: int, max_diff: int) -> np.ndarray:
+    img = np.array(img, dtype=np.int16, copy=True, order="C")
+    h, w = img.shape
+    lib().orc_filter_speckles_s16(_p(img, ctypes.c_int16), w, h, new_val, max_size, max_diff)
+    return img
+
+
+def reproject(disp_f32: np.ndarray, Q: np.ndarray, handle_missing: bool = False) -> np.ndarray:
+    disp_f32 = np.ascontiguousarray(disp_f32, dtype=np.float32)
+    Q = np.ascontiguousarray(Q, dtype=np.float64).reshape(16)
+    h, w = disp_f32.shape
+    out = np.empty((h, w, 3), np.float32)
+    lib().orc_reproject_f32(_p(disp_f32, ctypes.c_float), w, h, _p(Q, ctypes.c_double),
+                            int(bool(handle_missing)), _p(out, ctypes.c_float))
+    return out
+
+
+def bgr2gray(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w, _ = bgr.shape
+    out = np.empty((h, w), np.uint8)
+    lib().orc_bgr2gray(_p(bgr, ctypes.c_uint8), w, h, w * 3, _p(out, ctypes.c_uint8))
+    return out
+
+
+def resize_area_half(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape
+    out = np.empty((h // 2, w // 2), np.uint8)
+    lib().orc_resize_area_half(_p(src, ctypes.c_uint8), w, h, w, _p(out, ctypes.c_uint8))
+    return out
+
+
+def disp_to_float(disp: np.ndarray) -> np.ndarray:
+    disp = np.ascontiguousarray(disp, dtype=np.int16)
+    out = np.empty(disp.shape, np.float32)
+    lib().orc_disp_to_float(_p(disp, ctypes.c_int16), disp.size, _p(out, ctypes.c_float))
+    return out

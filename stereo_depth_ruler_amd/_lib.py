@@ -1,0 +1,98 @@
+"""ctypes binding of the engine's C ABI (include/sdr/sdr.h -> lib/libsdr.so).
+
+There is no CPU fallback: if the HIP library is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsdr.so")
+
+SDR_OK = 0
+ERRORS = {
+    -1: "SDR_ERR_ARG", -2: "SDR_ERR_NUMDISP", -3: "SDR_ERR_MODE", -4: "SDR_ERR_SIZE",
+    -5: "SDR_ERR_TYPE", -6: "SDR_ERR_DEVICE", -7: "SDR_ERR_NOMEM", -8: "SDR_ERR_LIMIT",
+}
+
+
+class SDRError(RuntimeError):
+    """Raised where cv::StereoSGBM / reprojectImageTo3D would throw cv::Exception."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class SgbmParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "minDisparity", "numDisparities", "blockSize", "P1", "P2", "disp12MaxDiff",
+        "preFilterCap", "uniquenessRatio", "speckleWindowSize", "speckleRange", "mode",
+        "nstripes", "uniq_rule")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+# (name, restype, argtypes) for every function declared in include/sdr/sdr.h
+_c = ctypes
+_vp = _c.c_void_p
+_sz = _c.c_size_t
+_i = _c.c_int
+_PP = _c.POINTER(SgbmParams)
+SIGNATURES = [
+    ("sdr_sgbm_params_default", None, [_PP]),
+    ("sdr_right_matcher_params", None, [_PP, _PP]),
+    ("sdr_sgbm_create", _i, [_PP, _i, _c.POINTER(_vp)]),
+    ("sdr_sgbm_destroy", _i, [_vp]),
+    ("sdr_sgbm_set_params", _i, [_vp, _PP]),
+    ("sdr_sgbm_get_params", _i, [_vp, _PP]),
+    ("sdr_sgbm_set_stream", _i, [_vp, _vp]),
+    ("sdr_sgbm_get_stream", _vp, [_vp]),
+    ("sdr_sgbm_compute", _i, [_vp, _vp, _vp, _i, _i, _i, _sz, _vp, _sz]),
+    ("sdr_sgbm_compute_device", _i, [_vp, _vp, _vp, _i, _i, _sz, _sz, _i, _vp, _sz, _sz]),
+    ("sdr_sgbm_compute_reproject_device", _i,
+     [_vp, _vp, _vp, _i, _i, _sz, _sz, _i, _vp, _c.POINTER(_c.c_double), _i, _vp]),
+    ("sdr_reproject", _i, [_vp, _i, _i, _sz, _c.POINTER(_c.c_double), _i, _vp, _sz]),
+    ("sdr_reproject_device", _i, [_vp, _i, _i, _sz, _c.POINTER(_c.c_double), _i, _vp, _sz, _i, _vp]),
+    ("sdr_disp16_reproject_device", _i,
+     [_vp, _i, _i, _sz, _c.POINTER(_c.c_double), _i, _vp, _sz, _i, _vp]),
+    ("sdr_disp16_to_float_device", _i, [_vp, _vp, _sz, _vp]),
+    ("sdr_bgr2gray_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
+    ("sdr_resize_area_half_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
+    ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),
+    ("sdr_sgbm_enable_timing", _i, [_vp, _i]),
+    ("sdr_sgbm_last_timing", _i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),
+                                  _c.POINTER(_c.c_float)]),
+    ("sdr_selftest_wave_ops", _i, [_c.POINTER(_c.c_int)]),
+    ("sdr_sgbm_debug_stage", _i, [_vp, _i, _vp, _sz]),
+    ("sdr_sgbm_kernel_time", _i, [_vp, _i, _i, _c.POINTER(_c.c_float), _c.POINTER(_c.c_int)]),
+    ("sdr_last_error", _c.c_char_p, []),
+    ("sdr_abi_version", _i, []),
+]
+
+
+def lib():
+    """Loads lib/libsdr.so (raises if the HIP extension has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"HIP engine library missing: {LIB_PATH}. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950).")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != SDR_OK:
+        raise SDRError(rc, lib().sdr_last_error().decode(errors="replace"))
+    return rc

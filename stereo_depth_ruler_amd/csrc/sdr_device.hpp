@@ -1,0 +1,94 @@
+// sdr_device.hpp -- CDNA4 (gfx950) device helpers for the stereo disparity engine.
+//
+// Costs and path values are int16 (OpenCV's CostType = short).  A 32-bit VGPR holds a packed
+// pair of disparities (lo = d, hi = d + 1) so one v_pk_{add,sub,min,max}_i16 advances two
+// disparities; a wave64 covers 64 * DPL disparities of one pixel.  Neighbours d-1 / d+1 across
+// lanes come from DPP wave_shr:1 / wave_shl:1 moves + v_alignbit, and per-pixel minima from
+// DPP butterflies + v_permlane{16,32}_swap (all in-register, no LDS).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdr {
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kMaxCost = 32767;
+constexpr uint32_t kMaxPair = 0x7fff7fffu;
+
+__device__ __forceinline__ s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return as_u32(as_s16x2(a) + as_s16x2(b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    return as_u32(as_s16x2(a) - as_s16x2(b));
+}
+__device__ __forceinline__ uint32_t pk_add_sat(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_add_sat(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_min(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_max(as_s16x2(a), as_s16x2(b)));
+}
+__device__ __forceinline__ uint32_t splat16(int v) {
+    return (uint32_t)(v & 0xffff) * 0x00010001u;
+}
+// {hi:lo} = {b.lo : a.hi}  i.e. (a >> 16) | (b << 16)
+__device__ __forceinline__ uint32_t funnel16(uint32_t b, uint32_t a) {
+    return __builtin_amdgcn_alignbit(b, a, 16);
+}
+
+// DPP controls (GFX9 encoding)
+constexpr int kDppQuadXor1 = 0xB1;      // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;      // quad_perm [2,3,0,1]
+constexpr int kDppRowHalfMirror = 0x141;
+constexpr int kDppRowMirror = 0x140;
+constexpr int kDppWaveShl1 = 0x130;     // lane i <- lane i+1
+constexpr int kDppWaveShr1 = 0x138;     // lane i <- lane i-1
+
+// lane i receives lane i-1's value; lane 0 receives `fill`
+__device__ __forceinline__ uint32_t lane_from_prev(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, kDppWaveShr1, 0xf, 0xf, false);
+}
+// lane i receives lane i+1's value; lane 63 receives `fill`
+__device__ __forceinline__ uint32_t lane_from_next(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, kDppWaveShl1, 0xf, 0xf, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+// Packed-int16 minimum over all 64 lanes, broadcast to every lane (both halves hold the same
+// value when the input's halves do).
+__device__ __forceinline__ uint32_t wave_min_pk(uint32_t m) {
+    m = pk_min(m, dpp_mov<kDppQuadXor1>(m));
+    m = pk_min(m, dpp_mov<kDppQuadXor2>(m));
+    m = pk_min(m, dpp_mov<kDppRowHalfMirror>(m));
+    m = pk_min(m, dpp_mov<kDppRowMirror>(m));
+    auto p16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+    m = pk_min(p16[0], p16[1]);
+    auto p32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+    return pk_min(p32[0], p32[1]);
+}
+
+// Unsigned 32-bit minimum over all 64 lanes, broadcast.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
+    m = min(m, dpp_mov<kDppQuadXor1>(m));
+    m = min(m, dpp_mov<kDppQuadXor2>(m));
+    m = min(m, dpp_mov<kDppRowHalfMirror>(m));
+    m = min(m, dpp_mov<kDppRowMirror>(m));
+    auto p16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
+    m = min((uint32_t)p16[0], (uint32_t)p16[1]);
+    auto p32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+    return min((uint32_t)p32[0], (uint32_t)p32[1]);
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+}  // namespace sdr

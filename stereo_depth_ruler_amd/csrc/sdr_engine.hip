@@ -1,0 +1,671 @@
+// sdr_engine.hip -- engine handle, scheduling of the stage kernels and the C ABI (include/sdr/sdr.h).
+//
+// One handle = one HIP stream + device scratch sized for the largest (W, H, D, frames) seen.
+// compute_device() enqueues the whole hot path of cv::StereoSGBM::compute on the stream:
+//   prefilter -> cost volume (+ 3WAY stripe-start rows) -> path kernels (first writes S, middle
+//   ones accumulate, last one fuses WTA/uniqueness/subpixel) -> disp2 + LR check -> median3
+//   -> speckle CCL [-> min -> reprojectImageTo3D]
+// No host synchronisation, allocation or copy happens inside the enqueue once scratch is sized,
+// so the sequence can be captured into a hipGraph by the caller.
+#include "../../include/sdr/sdr.h"
+#include "sdr_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define SDR_HIP(call)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (call);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(SDR_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Eff {
+    sdr::Geometry g;
+    int mode, uniq, uniq_simd, disp12MaxDiff, ftzero, nstripes, invalid;
+    int speckle_ws, speckle_diff, blockSize;
+};
+
+// OpenCV's parameter defaulting (stereosgbm.cpp computeDisparitySGBM / SGBM3WayMainLoop ctor).
+int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
+    if (p.numDisparities <= 0 || p.numDisparities % 16 != 0)
+        return fail(SDR_ERR_NUMDISP, "numDisparities must be positive and divisible by 16");
+    if (p.numDisparities > 256) return fail(SDR_ERR_LIMIT, "numDisparities > 256 is not supported");
+    if (p.mode != SDR_MODE_SGBM && p.mode != SDR_MODE_HH && p.mode != SDR_MODE_SGBM_3WAY)
+        return fail(SDR_ERR_MODE, "unsupported mode (MODE_HH4 is not implemented)");
+    sdr::Geometry& g = e->g;
+    g.W = W;
+    g.H = H;
+    g.D = p.numDisparities;
+    g.minD = p.minDisparity;
+    int maxD = g.minD + g.D;
+    g.minX1 = std::max(maxD, 0);
+    g.W1 = W + std::min(g.minD, 0) - g.minX1;
+    if (p.mode == SDR_MODE_SGBM_3WAY) {
+        g.SW2 = g.SH2 = p.blockSize > 0 ? p.blockSize / 2 : 1;
+    } else {
+        int bs = p.blockSize > 0 ? p.blockSize : 5;
+        g.SW2 = g.SH2 = bs / 2;
+    }
+    g.P1 = p.P1 > 0 ? p.P1 : 2;
+    g.P2 = std::max(p.P2 > 0 ? p.P2 : 5, g.P1 + 1);
+    e->mode = p.mode;
+    e->uniq = p.uniquenessRatio >= 0 ? p.uniquenessRatio : 10;
+    if (e->uniq >= 100) return fail(SDR_ERR_ARG, "uniquenessRatio must be < 100");
+    e->disp12MaxDiff = p.disp12MaxDiff > 0 ? p.disp12MaxDiff : 1;
+    e->ftzero = std::max(p.preFilterCap, 15) | 1;
+    e->nstripes = p.nstripes > 0 ? p.nstripes : 4;
+    e->uniq_simd = p.uniq_rule == SDR_UNIQ_SIMD ? 1
+                 : p.uniq_rule == SDR_UNIQ_SCALAR ? 0
+                 : (p.mode == SDR_MODE_SGBM_3WAY ? 1 : 0);
+    e->invalid = (g.minD - 1) * 16;
+    e->speckle_ws = p.speckleWindowSize;
+    e->speckle_diff = 16 * p.speckleRange;
+    e->blockSize = p.blockSize;
+    if (g.SH2 > 10 || g.SW2 > 10) return fail(SDR_ERR_ARG, "blockSize > 21 is not supported");
+    if (g.P2 > 16383) return fail(SDR_ERR_ARG, "P2 too large for int16 path costs");
+    return SDR_OK;
+}
+
+struct Buf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+int ensure(Buf& b, size_t bytes) {
+    if (b.n >= bytes && b.p) return SDR_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (bytes == 0) return SDR_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(SDR_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    }
+    b.n = bytes;
+    return SDR_OK;
+}
+
+struct Stripe {
+    int s0, end, out0, aux_rows, ylim;
+};
+
+void stripes_of(const Eff& e, std::vector<Stripe>* out) {
+    out->clear();
+    const int H = e.g.H;
+    const int n = e.nstripes;
+    const int sz = (int)std::ceil(H / (double)n);
+    const int overlap = (e.blockSize / 2 + 1) + (int)std::ceil(0.1 * sz);
+    for (int s = 0; s < n; s++) {
+        Stripe st;
+        st.out0 = s * sz;
+        if (st.out0 >= H) break;
+        st.s0 = std::max(std::min(s * sz - overlap, H), 0);
+        st.end = std::min((s + 1) * sz, H);
+        st.ylim = std::max(H - 1 - e.g.SH2, st.s0);
+        if (st.s0 == 0) st.aux_rows = 0;
+        else if (st.ylim >= st.s0 + e.g.SH2) st.aux_rows = e.g.SH2;
+        else st.aux_rows = st.end - st.s0;
+        out->push_back(st);
+    }
+}
+
+}  // namespace
+
+struct sdr_sgbm {
+    sdr_sgbm_params p{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    Buf planes, C, S, Caux, wta, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
+    int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // per-kernel event pairs (timing level 2), harvested by sdr_sgbm_kernel_time
+    std::vector<hipEvent_t> kev;
+    std::vector<int> kkind;
+    size_t kused = 0;
+};
+
+namespace {
+// RAII event pair around one kernel launch when per-kernel timing is on.
+struct KTimer {
+    sdr_sgbm* h;
+    bool on;
+    KTimer(sdr_sgbm* h_, int kind) : h(h_), on(h_->timing >= 2) {
+        if (!on) return;
+        if (h->kused * 2 + 2 > h->kev.size()) {
+            hipEvent_t a = nullptr, b = nullptr;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
+            h->kev.push_back(a);
+            h->kev.push_back(b);
+            h->kkind.push_back(kind);
+        }
+        h->kkind[h->kused] = kind;
+        (void)hipEventRecord(h->kev[2 * h->kused], h->stream);
+    }
+    ~KTimer() {
+        if (!on) return;
+        (void)hipEventRecord(h->kev[2 * h->kused + 1], h->stream);
+        h->kused++;
+    }
+};
+}  // namespace
+
+static int choose_tx(const sdr::Geometry& g) {
+    int TX = g.D <= 128 ? 32 : 16;
+    while (TX > 4 && sdr::cost_lds_bytes(g, TX) > 64 * 1024) TX /= 2;
+    return TX;
+}
+
+static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
+    const sdr::Geometry& g = e.g;
+    const size_t cells = (size_t)g.H * std::max(g.W1, 0) * g.D;
+    size_t aux = 0;
+    if (e.mode == SDR_MODE_SGBM_3WAY) {
+        stripes_of(e, st);
+        int amax = 0;
+        for (auto& s : *st) amax = std::max(amax, s.aux_rows);
+        aux = (size_t)st->size() * amax * std::max(g.W1, 0) * g.D * 2;
+    }
+    const size_t px = (size_t)g.W * g.H;
+    return (size_t)F * (2 * px * 8 + cells * 2 * 2 + aux + (size_t)g.H * std::max(g.W1, 0) * 4 +
+                        px * 2 * 3 + px * 4 * 2);
+}
+
+// Enqueues the full compute for F frames whose inputs are already on the device.
+static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
+                           size_t stride, size_t fstride, int F, int16_t** final_disp) {
+    Eff e;
+    int rc = make_eff(h->p, W, H, &e);
+    if (rc) return rc;
+    const sdr::Geometry& g = e.g;
+    hipStream_t st = h->stream;
+    const size_t px = (size_t)W * H;
+    if ((rc = ensure(h->dfin, F * px * 2))) return rc;
+    int16_t* dfin = (int16_t*)h->dfin.p;
+    *final_disp = dfin;
+    if (g.W1 <= 0) {
+        sdr::launch_fill_s16(dfin, (int16_t)e.invalid, F * px, st);
+        return SDR_OK;
+    }
+    if (g.W1 <= g.SW2) return fail(SDR_ERR_SIZE, "image too narrow for numDisparities/blockSize");
+    if (W > 8192) return fail(SDR_ERR_SIZE, "width > 8192 is not supported");
+
+    const size_t cells = (size_t)H * g.W1 * g.D;
+    std::vector<Stripe> stripes;
+    if (e.mode == SDR_MODE_SGBM_3WAY) stripes_of(e, &stripes);
+    int amax = 0;
+    for (auto& s : stripes) amax = std::max(amax, s.aux_rows);
+    const size_t aux_fstride = (size_t)stripes.size() * amax * g.W1 * g.D;
+
+    if ((rc = ensure(h->planes, F * 2 * px * 8))) return rc;
+    if ((rc = ensure(h->C, F * cells * 2))) return rc;
+    if ((rc = ensure(h->S, F * cells * 2))) return rc;
+    if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
+    if ((rc = ensure(h->wta, F * (size_t)H * g.W1 * 4))) return rc;
+    if ((rc = ensure(h->draw, F * px * 2))) return rc;
+    if ((rc = ensure(h->dlr, F * px * 2))) return rc;
+    if (e.speckle_ws > 0) {
+        if ((rc = ensure(h->labels, F * px * 4))) return rc;
+        if ((rc = ensure(h->sizes, F * px * 4))) return rc;
+    }
+
+    if (h->timing) SDR_HIP(hipEventRecord(h->ev[0], st));
+    uint64_t* planes = (uint64_t*)h->planes.p;
+    int16_t* C = (int16_t*)h->C.p;
+    int16_t* S = (int16_t*)h->S.p;
+    int16_t* Caux = (int16_t*)h->Caux.p;
+    uint32_t* wta = (uint32_t*)h->wta.p;
+    int16_t* draw = (int16_t*)h->draw.p;
+    int16_t* dlr = (int16_t*)h->dlr.p;
+
+    sdr::launch_fill_s16(draw, (int16_t)e.invalid, F * px, st);
+    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, planes, st); }
+
+    sdr::CostArgs ca{};
+    ca.planes = planes;
+    ca.planes_fstride = 2 * px;
+    ca.out = C;
+    ca.out_fstride = cells;
+    ca.out_row0 = 0;
+    ca.row_begin = 0;
+    ca.row_end = H;
+    ca.s0 = 0;
+    ca.ylim = std::max(H - 1 - g.SH2, 0);
+    ca.hh_bottom = e.mode == SDR_MODE_HH;
+    ca.TX = choose_tx(g);
+    ca.TY = 32;
+    { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
+    for (size_t s = 0; s < stripes.size(); s++) {
+        const Stripe& sp = stripes[s];
+        if (!sp.aux_rows) continue;
+        sdr::CostArgs xa = ca;
+        xa.out = Caux + s * (size_t)amax * g.W1 * g.D;
+        xa.out_fstride = aux_fstride;
+        xa.out_row0 = sp.s0;
+        xa.row_begin = sp.s0;
+        xa.row_end = sp.s0 + sp.aux_rows;
+        xa.s0 = sp.s0;
+        xa.ylim = sp.ylim;
+        xa.hh_bottom = 0;
+        xa.TY = sp.aux_rows;
+        KTimer kt(h, SDR_KERNEL_COST);
+        sdr::launch_cost(g, xa, F, st);
+    }
+    if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));
+
+    sdr::PathArgs pa{};
+    pa.C = C;
+    pa.S = S;
+    pa.cs_fstride = cells;
+    pa.disp_raw = draw;
+    pa.wta = wta;
+    pa.disp_fstride = px;
+    pa.wta_fstride = (size_t)H * g.W1;
+    pa.uniq = e.uniq;
+    pa.uniq_simd = e.uniq_simd;
+    pa.ybeg = 0;
+    pa.yend = H;
+    pa.write_from = 0;
+    const int nE = H, nS = g.W1, nD = g.W1 + H - 1;
+    auto run = [&](int dir, int smode, int nch) {
+        sdr::PathArgs q = pa;
+        q.dir = dir;
+        KTimer kt(h, SDR_KERNEL_PATH_WRITE + smode);
+        sdr::launch_path(g, q, smode, nch, F, st);
+    };
+    if (e.mode == SDR_MODE_SGBM) {
+        run(sdr::DIR_E, sdr::S_WRITE, nE);
+        run(sdr::DIR_SE, sdr::S_ADD, nD);
+        run(sdr::DIR_S, sdr::S_ADD, nS);
+        run(sdr::DIR_SW, sdr::S_ADD, nD);
+        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
+    } else if (e.mode == SDR_MODE_HH) {
+        run(sdr::DIR_E, sdr::S_WRITE, nE);
+        run(sdr::DIR_SE, sdr::S_ADD, nD);
+        run(sdr::DIR_S, sdr::S_ADD, nS);
+        run(sdr::DIR_SW, sdr::S_ADD, nD);
+        run(sdr::DIR_NE, sdr::S_ADD, nD);
+        run(sdr::DIR_N, sdr::S_ADD, nS);
+        run(sdr::DIR_NW, sdr::S_ADD, nD);
+        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
+    } else {
+        run(sdr::DIR_E, sdr::S_WRITE, nE);
+        for (size_t s = 0; s < stripes.size(); s++) {
+            const Stripe& sp = stripes[s];
+            sdr::PathArgs q = pa;
+            q.dir = sdr::DIR_S;
+            q.ybeg = sp.s0;
+            q.yend = sp.end;
+            q.write_from = sp.out0;
+            if (sp.aux_rows) {
+                q.Caux = Caux + s * (size_t)amax * g.W1 * g.D;
+                q.aux_fstride = aux_fstride;
+                q.aux_row0 = sp.s0;
+                q.aux_rows = sp.aux_rows;
+            }
+            KTimer kt(h, SDR_KERNEL_PATH_ADD);
+            sdr::launch_path(g, q, sdr::S_ADD, nS, F, st);
+        }
+        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
+    }
+    if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
+
+    sdr::LrArgs la{};
+    la.disp_raw = draw;
+    la.wta = wta;
+    la.out = dlr;
+    la.disp_fstride = px;
+    la.wta_fstride = (size_t)H * g.W1;
+    la.disp12MaxDiff = e.disp12MaxDiff;
+    { KTimer kt(h, SDR_KERNEL_LR); sdr::launch_lr(g, la, F, st); }
+    { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, dfin, W, H, F, st); }
+    if (e.speckle_ws > 0) {
+        KTimer kt(h, SDR_KERNEL_SPECKLE);
+        sdr::launch_speckle(dfin, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
+                            (int*)h->labels.p, (int*)h->sizes.p, st);
+    }
+    if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+// ===========================================================================================
+// C ABI
+// ===========================================================================================
+extern "C" {
+
+const char* sdr_last_error(void) { return g_last_error.c_str(); }
+int sdr_abi_version(void) { return SDR_ABI_VERSION; }
+
+void sdr_sgbm_params_default(sdr_sgbm_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->numDisparities = 16;
+    p->blockSize = 3;
+    p->mode = SDR_MODE_SGBM;
+    p->nstripes = 4;
+}
+
+void sdr_right_matcher_params(const sdr_sgbm_params* l, sdr_sgbm_params* r) {
+    if (!l || !r) return;
+    // ximgproc createRightMatcher: StereoSGBM::create(-(min+num)+1, num, wsize) + setters
+    sdr_sgbm_params_default(r);
+    r->minDisparity = -(l->minDisparity + l->numDisparities) + 1;
+    r->numDisparities = l->numDisparities;
+    r->blockSize = l->blockSize;
+    r->uniquenessRatio = 0;
+    r->P1 = l->P1;
+    r->P2 = l->P2;
+    r->mode = l->mode;
+    r->preFilterCap = l->preFilterCap;
+    r->disp12MaxDiff = 1000000;
+    r->speckleWindowSize = 0;
+    r->speckleRange = l->speckleRange;
+    r->nstripes = l->nstripes;
+    r->uniq_rule = l->uniq_rule;
+}
+
+int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out) {
+    if (!p || !out) return fail(SDR_ERR_ARG, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    SDR_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SDR_ERR_DEVICE, "invalid device index");
+    SDR_HIP(hipSetDevice(device));
+    sdr_sgbm* h = new sdr_sgbm();
+    h->p = *p;
+    h->device = device;
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(SDR_ERR_DEVICE, "hipStreamCreate failed");
+    }
+    h->stream = h->own_stream;
+    for (auto& ev : h->ev) (void)hipEventCreate(&ev);
+    *out = h;
+    return SDR_OK;
+}
+
+int sdr_sgbm_destroy(sdr_sgbm* h) {
+    if (!h) return SDR_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (Buf* b : {&h->planes, &h->C, &h->S, &h->Caux, &h->wta, &h->draw, &h->dlr, &h->dfin,
+                   &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz})
+        if (b->p) (void)hipFree(b->p);
+    for (auto ev : h->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto ev : h->kev) (void)hipEventDestroy(ev);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+    return SDR_OK;
+}
+
+int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p) {
+    if (!h || !p) return fail(SDR_ERR_ARG, "null argument");
+    h->p = *p;
+    return SDR_OK;
+}
+
+int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p) {
+    if (!h || !p) return fail(SDR_ERR_ARG, "null argument");
+    *p = h->p;
+    return SDR_OK;
+}
+
+int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    return SDR_OK;
+}
+
+void* sdr_sgbm_get_stream(const sdr_sgbm* h) { return h ? (void*)h->stream : nullptr; }
+
+int sdr_sgbm_enable_timing(sdr_sgbm* h, int enable) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    h->timing = enable < 0 ? 0 : enable;
+    h->kused = 0;
+    return SDR_OK;
+}
+
+int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms) {
+    if (!h || !h->timing) return fail(SDR_ERR_ARG, "timing not enabled");
+    SDR_HIP(hipEventSynchronize(h->ev[3]));
+    float a = 0, b = 0, c = 0;
+    SDR_HIP(hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
+    SDR_HIP(hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+    SDR_HIP(hipEventElapsedTime(&c, h->ev[2], h->ev[3]));
+    if (cost_ms) *cost_ms = a;
+    if (paths_ms) *paths_ms = b;
+    if (post_ms) *post_ms = c;
+    return SDR_OK;
+}
+
+size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes) {
+    if (!p) return 0;
+    Eff e;
+    if (make_eff(*p, width, height, &e)) return 0;
+    std::vector<Stripe> st;
+    return scratch_bytes(e, std::max(nframes, 1), &st);
+}
+
+static int check_dims(int W, int H, size_t stride, int F) {
+    if (W <= 0 || H <= 0 || F <= 0) return fail(SDR_ERR_ARG, "non-positive size");
+    if (stride < (size_t)W) return fail(SDR_ERR_ARG, "stride < width");
+    return SDR_OK;
+}
+
+int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, int W, int H,
+                            size_t stride, size_t fstride, int F, int16_t* dDisp,
+                            size_t disp_stride, size_t disp_fstride) {
+    if (!h || !dL || !dR || !dDisp) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, stride, F);
+    if (rc) return rc;
+    if (disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
+    if (F > 1 && fstride < stride * H) return fail(SDR_ERR_ARG, "frame_stride too small");
+    SDR_HIP(hipSetDevice(h->device));
+    int16_t* fin = nullptr;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, &fin))) return rc;
+    const size_t px = (size_t)W * H;
+    if (disp_stride == (size_t)W && (F == 1 || disp_fstride == px)) {
+        SDR_HIP(hipMemcpyAsync(dDisp, fin, F * px * 2, hipMemcpyDeviceToDevice, h->stream));
+    } else {
+        for (int f = 0; f < F; f++)
+            SDR_HIP(hipMemcpy2DAsync(dDisp + f * disp_fstride, disp_stride * 2, fin + f * px, W * 2,
+                                     W * 2, H, hipMemcpyDeviceToDevice, h->stream));
+    }
+    return SDR_OK;
+}
+
+int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, int W,
+                                      int H, size_t stride, size_t fstride, int F, int16_t* dDisp,
+                                      const double Q[16], int handle_missing, float* dXYZ) {
+    if (!h || !dL || !dR || !Q || !dXYZ) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, stride, F);
+    if (rc) return rc;
+    if (F > 1 && fstride < stride * H) return fail(SDR_ERR_ARG, "frame_stride too small");
+    SDR_HIP(hipSetDevice(h->device));
+    int16_t* fin = nullptr;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, &fin))) return rc;
+    const size_t px = (size_t)W * H;
+    if ((rc = ensure(h->mins, (size_t)F * 4))) return rc;
+    {
+        KTimer kt(h, SDR_KERNEL_REPROJECT);
+        if (handle_missing) sdr::launch_min_s16(fin, px, px, F, (int*)h->mins.p, h->stream);
+        sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, (const int*)h->mins.p, dXYZ,
+                                  (size_t)W * 3, px * 3, F, h->stream);
+    }
+    if (dDisp) SDR_HIP(hipMemcpyAsync(dDisp, fin, F * px * 2, hipMemcpyDeviceToDevice, h->stream));
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int W, int H,
+                     int channels, size_t stride, int16_t* disp, size_t disp_stride) {
+    if (!h || !left || !right || !disp) return fail(SDR_ERR_ARG, "null argument");
+    if (channels != 1) return fail(SDR_ERR_TYPE, "only 8-bit single-channel images are supported");
+    int rc = check_dims(W, H, stride, 1);
+    if (rc) return rc;
+    if (disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
+    SDR_HIP(hipSetDevice(h->device));
+    const size_t px = (size_t)W * H;
+    if ((rc = ensure(h->hin, 2 * px))) return rc;
+    uint8_t* dL = (uint8_t*)h->hin.p;
+    uint8_t* dR = dL + px;
+    SDR_HIP(hipMemcpy2DAsync(dL, W, left, stride, W, H, hipMemcpyHostToDevice, h->stream));
+    SDR_HIP(hipMemcpy2DAsync(dR, W, right, stride, W, H, hipMemcpyHostToDevice, h->stream));
+    int16_t* fin = nullptr;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, &fin))) return rc;
+    SDR_HIP(hipMemcpy2DAsync(disp, disp_stride * 2, fin, W * 2, W * 2, H, hipMemcpyDeviceToHost,
+                             h->stream));
+    SDR_HIP(hipStreamSynchronize(h->stream));
+    return SDR_OK;
+}
+
+int sdr_reproject_device(const float* d_disp, int W, int H, size_t disp_stride, const double Q[16],
+                         int handle_missing, float* d_xyz, size_t xyz_stride, int F,
+                         void* stream) {
+    if (!d_disp || !Q || !d_xyz) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, disp_stride, F);
+    if (rc) return rc;
+    if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
+    int* mins = nullptr;
+    if (handle_missing) SDR_HIP(hipMallocAsync((void**)&mins, F * sizeof(int), (hipStream_t)stream));
+    sdr::launch_reproject_f32(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,
+                              d_xyz, xyz_stride, xyz_stride * H, F, (hipStream_t)stream);
+    if (mins) SDR_HIP(hipFreeAsync(mins, (hipStream_t)stream));
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_disp16_reproject_device(const int16_t* d_disp, int W, int H, size_t disp_stride,
+                                const double Q[16], int handle_missing, float* d_xyz,
+                                size_t xyz_stride, int F, void* stream) {
+    if (!d_disp || !Q || !d_xyz) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, disp_stride, F);
+    if (rc) return rc;
+    if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
+    if (handle_missing && disp_stride != (size_t)W)
+        return fail(SDR_ERR_ARG, "handle_missing needs a dense disparity (disp_stride == width)");
+    int* mins = nullptr;
+    hipStream_t st = (hipStream_t)stream;
+    if (handle_missing) {
+        SDR_HIP(hipMallocAsync((void**)&mins, F * sizeof(int), st));
+        sdr::launch_min_s16(d_disp, (size_t)W * H, disp_stride * H, F, mins, st);
+    }
+    sdr::launch_reproject_s16(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,
+                              d_xyz, xyz_stride, xyz_stride * H, F, st);
+    if (mins) SDR_HIP(hipFreeAsync(mins, st));
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_reproject(const float* disp, int W, int H, size_t disp_stride, const double Q[16],
+                  int handle_missing, float* xyz, size_t xyz_stride) {
+    if (!disp || !Q || !xyz) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, disp_stride, 1);
+    if (rc) return rc;
+    if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
+    const size_t px = (size_t)W * H;
+    float *dd = nullptr, *dx = nullptr;
+    SDR_HIP(hipMalloc(&dd, px * 4));
+    if (hipMalloc(&dx, px * 12) != hipSuccess) {
+        (void)hipFree(dd);
+        return fail(SDR_ERR_NOMEM, "hipMalloc failed");
+    }
+    rc = SDR_OK;
+    if (hipMemcpy2D(dd, W * 4, disp, disp_stride * 4, W * 4, H, hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(SDR_ERR_DEVICE, "H2D failed");
+    if (!rc) rc = sdr_reproject_device(dd, W, H, W, Q, handle_missing, dx, (size_t)W * 3, 1, nullptr);
+    if (!rc && hipMemcpy2D(xyz, xyz_stride * 4, dx, (size_t)W * 12, (size_t)W * 12, H,
+                           hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(SDR_ERR_DEVICE, "D2H failed");
+    (void)hipFree(dd);
+    (void)hipFree(dx);
+    return rc;
+}
+
+int sdr_disp16_to_float_device(const int16_t* d_disp, float* d_out, size_t n, void* stream) {
+    if (!d_disp || !d_out) return fail(SDR_ERR_ARG, "null argument");
+    sdr::launch_disp16_to_f32(d_disp, d_out, n, (hipStream_t)stream);
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_bgr2gray_device(const uint8_t* d_bgr, int W, int H, size_t bgr_stride, uint8_t* d_gray,
+                        size_t gray_stride, int F, void* stream) {
+    if (!d_bgr || !d_gray) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, gray_stride, F);
+    if (rc) return rc;
+    if (bgr_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "bgr_stride < 3*width");
+    sdr::launch_bgr2gray(d_bgr, W, H, bgr_stride, d_gray, gray_stride, F, (hipStream_t)stream);
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_resize_area_half_device(const uint8_t* d_src, int W, int H, size_t stride, uint8_t* d_dst,
+                                size_t dst_stride, int F, void* stream) {
+    if (!d_src || !d_dst) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, stride, F);
+    if (rc) return rc;
+    if ((W & 1) || (H & 1)) return fail(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
+    if (dst_stride < (size_t)W / 2) return fail(SDR_ERR_ARG, "dst_stride < width/2");
+    sdr::launch_area_half(d_src, W, H, stride, d_dst, dst_stride, F, (hipStream_t)stream);
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int* count) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    float tot = 0;
+    int n = 0;
+    if (h->kused) {
+        SDR_HIP(hipEventSynchronize(h->kev[2 * h->kused - 1]));
+        for (size_t i = 0; i < h->kused; i++) {
+            if (kind >= 0 && h->kkind[i] != kind) continue;
+            float ms = 0;
+            SDR_HIP(hipEventElapsedTime(&ms, h->kev[2 * i], h->kev[2 * i + 1]));
+            tot += ms;
+            n++;
+        }
+    }
+    if (total_ms) *total_ms = tot;
+    if (count) *count = n;
+    if (reset) h->kused = 0;
+    return SDR_OK;
+}
+
+int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) {
+    if (!h || !dst) return fail(SDR_ERR_ARG, "null argument");
+    const Buf* b = stage == 0 ? &h->C : stage == 1 ? &h->draw : stage == 2 ? &h->dlr
+                 : stage == 3 ? &h->dfin : stage == 4 ? &h->wta : nullptr;
+    if (!b) return fail(SDR_ERR_ARG, "bad stage");
+    if (!b->p || bytes > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
+    SDR_HIP(hipSetDevice(h->device));
+    SDR_HIP(hipStreamSynchronize(h->stream));
+    SDR_HIP(hipMemcpy(dst, b->p, bytes, hipMemcpyDeviceToHost));
+    return SDR_OK;
+}
+
+int sdr_selftest_wave_ops(int* failures4) {
+    if (!failures4) return fail(SDR_ERR_ARG, "null argument");
+    return sdr::selftest_wave_ops(failures4) ? fail(SDR_ERR_DEVICE, "selftest launch failed") : SDR_OK;
+}
+
+}  // extern "C"

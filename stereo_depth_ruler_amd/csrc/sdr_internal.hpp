@@ -1,0 +1,97 @@
+// sdr_internal.hpp -- launchers shared between sdr_kernels.hip and sdr_engine.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdr {
+
+// Scanline directions of the path recurrence.  dx/dy = step between
+// consecutive pixels of one chain.
+enum Dir : int {
+    DIR_E = 0,   // -> (x ascending)        OpenCV dir 0, pass 1
+    DIR_W = 1,   // <- (x descending)       OpenCV dir 4 (SGBM/3WAY), dir 0 pass 2 (HH)
+    DIR_S = 2,   // top -> bottom           dir 2 pass 1
+    DIR_N = 3,   // bottom -> top           dir 2 pass 2 (HH)
+    DIR_SE = 4,  // (x-1,y-1) -> (x,y)      dir 1 pass 1
+    DIR_SW = 5,  // (x+1,y-1) -> (x,y)      dir 3 pass 1
+    DIR_NE = 6,  // (x-1,y+1) -> (x,y)      dir 1 pass 2 (HH)
+    DIR_NW = 7,  // (x+1,y+1) -> (x,y)      dir 3 pass 2 (HH)
+};
+
+enum SMode : int { S_WRITE = 0, S_ADD = 1, S_ADD_WTA = 2 };
+
+struct Geometry {
+    int W, H;           // image size
+    int D, minD;        // disparity count / minimum
+    int minX1, W1;      // matched column range [minX1, minX1 + W1)
+    int SW2, SH2;       // block half sizes
+    int P1, P2;
+};
+
+struct CostArgs {
+    const uint64_t* planes;  // [F][2][H][W] BT planes (left, right)
+    size_t planes_fstride;   // elements per frame
+    int16_t* out;            // cost rows
+    size_t out_fstride;      // elements per frame
+    int out_row0;            // row index of out's first row
+    int row_begin, row_end;  // output rows [row_begin, row_end)
+    int s0;                  // chain/box start row (box clamp)
+    int ylim;                // rows > ylim repeat row ylim (running sum stops updating)
+    int hh_bottom;           // MODE_HH: rows y>0 with y+SH2>=H keep the initial P2
+    int TX;                  // tile width (matched columns)
+    int TY;                  // tile height (output rows)
+};
+
+struct PathArgs {
+    const int16_t* C;        // [F][H][W1][D]
+    int16_t* S;              // [F][H][W1][D]
+    const int16_t* Caux;     // 3WAY stripe-start rows [F][aux_rows][W1][D] or null
+    size_t cs_fstride;       // elements per frame of C/S
+    size_t aux_fstride;
+    int aux_row0, aux_rows;
+    int dir;
+    int ybeg, yend;          // vertical chain row range (DIR_S): [ybeg, yend)
+    int write_from;          // DIR_S: first row whose S is written (3WAY stripe output start)
+    // WTA (S_ADD_WTA)
+    int16_t* disp_raw;       // [F][H][W] int16 (matched columns written)
+    uint32_t* wta;           // [F][H][W1] (minS << 16 | best) or 0xffffffff
+    size_t disp_fstride, wta_fstride;
+    int uniq, uniq_simd;
+};
+
+struct LrArgs {
+    const int16_t* disp_raw; // [F][H][W]
+    const uint32_t* wta;     // [F][H][W1]
+    int16_t* out;            // [F][H][W]
+    size_t disp_fstride, wta_fstride;
+    int disp12MaxDiff;
+};
+
+void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st);
+void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
+                      int H, int F, int ftzero, uint64_t* planes, hipStream_t st);
+int cost_lds_bytes(const Geometry& g, int TX);
+void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
+void launch_path(const Geometry& g, const PathArgs& a, int smode, int nchains, int F,
+                 hipStream_t st);
+void launch_lr(const Geometry& g, const LrArgs& a, int F, hipStream_t st);
+void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
+void launch_speckle(int16_t* img, int W, int H, int F, int newVal, int maxSize, int maxDiff,
+                    int* labels, int* sizes, hipStream_t st);
+void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
+                    hipStream_t st);
+void launch_reproject_s16(const int16_t* disp, int W, int H, size_t dstride, size_t dfstride,
+                          const double* Q, int handle_missing, const int* mins, float* xyz,
+                          size_t xyz_stride, size_t xyz_fstride, int F, hipStream_t st);
+void launch_reproject_f32(const float* disp, int W, int H, size_t dstride, size_t dfstride,
+                          const double* Q, int handle_missing, int* minbits_scratch, float* xyz,
+                          size_t xyz_stride, size_t xyz_fstride, int F, hipStream_t st);
+void launch_disp16_to_f32(const int16_t* d, float* o, size_t n, hipStream_t st);
+void launch_bgr2gray(const uint8_t* bgr, int W, int H, size_t bstride, uint8_t* gray,
+                     size_t gstride, int F, hipStream_t st);
+void launch_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* dst,
+                      size_t dstride, int F, hipStream_t st);
+int selftest_wave_ops(int* failures);
+
+}  // namespace sdr

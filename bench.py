@@ -118,6 +118,7 @@ def main():
 
     import stereo_depth_ruler_amd as sdr
     from stereo_depth_ruler_amd import synthetic as S
+    from stereo_depth_ruler_amd.distributed import as_bytes
     from stereo_depth_ruler_amd.sgbm import KERNEL_PATH_ADD
 
     desc, W, H, args, batch, hm = CONFIGS[a.config]
@@ -130,8 +131,9 @@ def main():
     disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
     xyz = torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev)
     gather_bufs = None
-    if world > 1 and rank == 0:
-        gather_bufs = [[torch.empty_like(disp[0]) for _ in range(world)] for _ in range(2)]
+    if world > 1 and rank == 0:  # RCCL has no int16: gather the disparity bytes
+        gather_bufs = [[torch.empty(batch * H * W * 2, dtype=torch.uint8, device=dev) for _ in range(world)]
+                       for _ in range(2)]
     pending = [None, None]
 
     def step(i):
@@ -142,8 +144,8 @@ def main():
             pending[slot] = None
         m.compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot], xyz=xyz)
         if world > 1:
-            pending[slot] = dist.gather(disp[slot], gather_bufs[slot] if rank == 0 else None, dst=0,
-                                        async_op=True)
+            pending[slot] = dist.gather(as_bytes(disp[slot]), gather_bufs[slot] if rank == 0 else None,
+                                        dst=0, async_op=True)
 
     for i in range(a.warmup):
         step(i)

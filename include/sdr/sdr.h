@@ -125,6 +125,16 @@ int sdr_bgr2gray_device(const uint8_t* d_bgr, int width, int height, size_t bgr_
 int sdr_resize_area_half_device(const uint8_t* d_src, int width, int height, size_t stride,
                                 uint8_t* d_dst, size_t dst_stride, int nframes, void* stream);
 
+/* StereoDisparity::computeDisparity class path (stereo_disparity.cpp:17-39) on host BGR frames:
+ * cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left->compute(L, R) [-> right->compute(R, L)]
+ * -> convertTo(CV_32F, 1/16), all on the left matcher's device.  out: float (height/2)x(width/2).
+ * The ximgproc WLS filter (stereo_disparity.cpp:31) is not applied yet:
+ * out is the left matcher's disparity; disp_left/disp_right (optional) receive the CV_16S maps. */
+int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr_left,
+                             const uint8_t* bgr_right, int width, int height, size_t bgr_stride,
+                             float* out, size_t out_stride, int16_t* disp_left,
+                             int16_t* disp_right);
+
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);
 

@@ -1,0 +1,235 @@
+// stereo.hpp -- header-only C++ facade over the C ABI (sdr.h) with the reference's C++ surface:
+//
+//   sdr::StereoSGBM::create(...) / compute(L, R, disp)      <- cv::StereoSGBM
+//       reference stereo_vision/src/stereo_disparity.cpp:5-9,27-28, point_cloud/src/pcd_write.cpp:102-111
+//   sdr::reprojectImageTo3D(disp, xyz, Q, handleMissing)    <- cv::reprojectImageTo3D
+//       stereo_disparity.cpp:78, pcd_write.cpp:116
+//   sdr::ximgproc::createRightMatcher(left)                 <- cv::ximgproc::createRightMatcher
+//   sdr::StereoDisparity                                     <- class StereoDisparity
+//       stereo_vision/include/stereo_disparity.hpp:8-24
+//
+// sdr::Mat is a minimal owning image (rows, cols, OpenCV type code, row step) so that callers
+// can switch from cv::Mat without OpenCV present; when OpenCV is available, wrap cv::Mat data
+// pointers with sdr::Mat::view(...) at zero cost.  Errors throw sdr::Exception (cf. cv::Exception).
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sdr.h"
+
+namespace sdr {
+
+enum { CV_8UC1 = 0, CV_16SC1 = 3, CV_32FC1 = 5, CV_64FC1 = 6, CV_8UC3 = 16, CV_32FC3 = 21 };
+
+inline size_t elem_size(int type) {
+    switch (type) {
+    case CV_8UC1: return 1;
+    case CV_16SC1: return 2;
+    case CV_32FC1: return 4;
+    case CV_64FC1: return 8;
+    case CV_8UC3: return 3;
+    case CV_32FC3: return 12;
+    default: throw std::invalid_argument("sdr::Mat: unsupported type");
+    }
+}
+
+class Exception : public std::runtime_error {
+public:
+    Exception(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}
+    int code;
+};
+
+inline void check(int rc) {
+    if (rc != SDR_OK) throw Exception(rc, sdr_last_error());
+}
+
+class Mat {
+public:
+    int rows = 0, cols = 0, type = CV_8UC1;
+    size_t step = 0;  // bytes per row
+    uint8_t* data = nullptr;
+
+    Mat() = default;
+    Mat(int r, int c, int t) { create(r, c, t); }
+    static Mat view(int r, int c, int t, void* p, size_t step_bytes = 0) {
+        Mat m;
+        m.rows = r; m.cols = c; m.type = t;
+        m.step = step_bytes ? step_bytes : (size_t)c * elem_size(t);
+        m.data = (uint8_t*)p;
+        return m;
+    }
+    void create(int r, int c, int t) {  // like cv::Mat::create: reallocates only when needed
+        if (data && r == rows && c == cols && t == type) return;
+        rows = r; cols = c; type = t;
+        step = (size_t)c * elem_size(t);
+        store_ = std::make_shared<std::vector<uint8_t>>((size_t)r * step);
+        data = store_->data();
+    }
+    bool empty() const { return !data || rows == 0 || cols == 0; }
+    template <typename T> T* ptr(int y) { return (T*)(data + (size_t)y * step); }
+    template <typename T> const T* ptr(int y) const { return (const T*)(data + (size_t)y * step); }
+    template <typename T> T& at(int y, int x) { return ptr<T>(y)[x]; }
+    Mat clone() const {
+        Mat m(rows, cols, type);
+        for (int y = 0; y < rows; y++) std::memcpy(m.ptr<uint8_t>(y), ptr<uint8_t>(y), (size_t)cols * elem_size(type));
+        return m;
+    }
+
+private:
+    std::shared_ptr<std::vector<uint8_t>> store_;
+};
+
+template <class T> using Ptr = std::shared_ptr<T>;
+
+class StereoSGBM {
+public:
+    enum { MODE_SGBM = SDR_MODE_SGBM, MODE_HH = SDR_MODE_HH, MODE_SGBM_3WAY = SDR_MODE_SGBM_3WAY,
+           MODE_HH4 = SDR_MODE_HH4 };
+
+    static Ptr<StereoSGBM> create(int minDisparity = 0, int numDisparities = 16, int blockSize = 3,
+                                  int P1 = 0, int P2 = 0, int disp12MaxDiff = 0, int preFilterCap = 0,
+                                  int uniquenessRatio = 0, int speckleWindowSize = 0,
+                                  int speckleRange = 0, int mode = MODE_SGBM, int device = 0) {
+        sdr_sgbm_params p;
+        sdr_sgbm_params_default(&p);
+        p.minDisparity = minDisparity; p.numDisparities = numDisparities; p.blockSize = blockSize;
+        p.P1 = P1; p.P2 = P2; p.disp12MaxDiff = disp12MaxDiff; p.preFilterCap = preFilterCap;
+        p.uniquenessRatio = uniquenessRatio; p.speckleWindowSize = speckleWindowSize;
+        p.speckleRange = speckleRange; p.mode = mode;
+        return Ptr<StereoSGBM>(new StereoSGBM(p, device));
+    }
+    static Ptr<StereoSGBM> create(const sdr_sgbm_params& p, int device = 0) {
+        return Ptr<StereoSGBM>(new StereoSGBM(p, device));
+    }
+    ~StereoSGBM() { sdr_sgbm_destroy(h_); }
+    StereoSGBM(const StereoSGBM&) = delete;
+    StereoSGBM& operator=(const StereoSGBM&) = delete;
+
+    // StereoMatcher::compute: CV_8UC1 pair -> CV_16SC1 disparity (1/16 px); disp is (re)allocated
+    void compute(const Mat& left, const Mat& right, Mat& disparity) {
+        if (left.rows != right.rows || left.cols != right.cols || left.type != right.type)
+            throw Exception(SDR_ERR_ARG, "left and right images must have the same size and type");
+        if (left.type != CV_8UC1 || left.step != right.step)
+            throw Exception(SDR_ERR_TYPE, "8-bit single-channel images with equal steps are required");
+        disparity.create(left.rows, left.cols, CV_16SC1);
+        check(sdr_sgbm_compute(h_, left.data, right.data, left.cols, left.rows, 1, left.step,
+                               (int16_t*)disparity.data, disparity.step / 2));
+    }
+
+    int getMinDisparity() const { return p_.minDisparity; }
+    void setMinDisparity(int v) { p_.minDisparity = v; push(); }
+    int getNumDisparities() const { return p_.numDisparities; }
+    void setNumDisparities(int v) { p_.numDisparities = v; push(); }
+    int getBlockSize() const { return p_.blockSize; }
+    void setBlockSize(int v) { p_.blockSize = v; push(); }
+    int getP1() const { return p_.P1; }
+    void setP1(int v) { p_.P1 = v; push(); }
+    int getP2() const { return p_.P2; }
+    void setP2(int v) { p_.P2 = v; push(); }
+    int getDisp12MaxDiff() const { return p_.disp12MaxDiff; }
+    void setDisp12MaxDiff(int v) { p_.disp12MaxDiff = v; push(); }
+    int getPreFilterCap() const { return p_.preFilterCap; }
+    void setPreFilterCap(int v) { p_.preFilterCap = v; push(); }
+    int getUniquenessRatio() const { return p_.uniquenessRatio; }
+    void setUniquenessRatio(int v) { p_.uniquenessRatio = v; push(); }
+    int getSpeckleWindowSize() const { return p_.speckleWindowSize; }
+    void setSpeckleWindowSize(int v) { p_.speckleWindowSize = v; push(); }
+    int getSpeckleRange() const { return p_.speckleRange; }
+    void setSpeckleRange(int v) { p_.speckleRange = v; push(); }
+    int getMode() const { return p_.mode; }
+    void setMode(int v) { p_.mode = v; push(); }
+
+    const sdr_sgbm_params& params() const { return p_; }
+    sdr_sgbm* handle() const { return h_; }
+    int device() const { return dev_; }
+
+private:
+    StereoSGBM(const sdr_sgbm_params& p, int device) : p_(p), dev_(device) {
+        check(sdr_sgbm_create(&p_, device, &h_));
+    }
+    void push() { check(sdr_sgbm_set_params(h_, &p_)); }
+    sdr_sgbm_params p_;
+    sdr_sgbm* h_ = nullptr;
+    int dev_ = 0;
+};
+
+// cv::reprojectImageTo3D(disparity CV_32F or CV_16S, _3dImage CV_32FC3, Q 4x4, handleMissing)
+// convertTo: disp.convertTo(f, CV_32F, 1/16) as the reference does before reprojecting
+inline void convertTo32F(const Mat& disp16, Mat& f, double scale) {
+    if (disp16.type != CV_16SC1) throw Exception(SDR_ERR_TYPE, "convertTo32F expects CV_16S");
+    f.create(disp16.rows, disp16.cols, CV_32FC1);
+    const float a = (float)scale;
+    for (int y = 0; y < disp16.rows; y++)
+        for (int x = 0; x < disp16.cols; x++) f.ptr<float>(y)[x] = (float)disp16.ptr<int16_t>(y)[x] * a;
+}
+
+inline void reprojectImageTo3D(const Mat& disparity, Mat& xyz, const Mat& Q,
+                               bool handleMissingValues = false) {
+    if (Q.rows != 4 || Q.cols != 4) throw Exception(SDR_ERR_ARG, "Q must be 4x4");
+    double q[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+            q[i * 4 + j] = Q.type == CV_64FC1 ? Q.ptr<double>(i)[j] : (double)Q.ptr<float>(i)[j];
+    Mat f = disparity;
+    if (disparity.type == CV_16SC1) {  // OpenCV reads CV_16S values as-is (no 1/16 scaling)
+        f = Mat(disparity.rows, disparity.cols, CV_32FC1);
+        for (int y = 0; y < disparity.rows; y++)
+            for (int x = 0; x < disparity.cols; x++) f.ptr<float>(y)[x] = (float)disparity.ptr<int16_t>(y)[x];
+    } else if (disparity.type != CV_32FC1) {
+        throw Exception(SDR_ERR_TYPE, "disparity must be CV_32F or CV_16S");
+    }
+    xyz.create(disparity.rows, disparity.cols, CV_32FC3);
+    check(sdr_reproject(f.ptr<float>(0), f.cols, f.rows, f.step / 4, q, handleMissingValues ? 1 : 0,
+                        xyz.ptr<float>(0), xyz.step / 4));
+}
+
+namespace ximgproc {
+// cv::ximgproc::createRightMatcher(matcher_left)
+inline Ptr<StereoSGBM> createRightMatcher(const Ptr<StereoSGBM>& left) {
+    sdr_sgbm_params r;
+    sdr_right_matcher_params(&left->params(), &r);
+    return StereoSGBM::create(r, left->device());
+}
+}  // namespace ximgproc
+
+// class StereoDisparity (reference stereo_vision/include/stereo_disparity.hpp:8-24)
+class StereoDisparity {
+public:
+    explicit StereoDisparity(const Mat& Q_matrix, int device = 0) : Q(Q_matrix.clone()) {
+        // stereo_disparity.cpp:5-9: StereoSGBM::create(0, 80, 5, 8*5*5*3, 32*5*5*3, 1, 63, 12, 200, 2, 3WAY)
+        matcher = StereoSGBM::create(0, 80, 5, 8 * 5 * 5 * 3, 32 * 5 * 5 * 3, 1, 63, 12, 200, 2,
+                                     StereoSGBM::MODE_SGBM_3WAY, device);
+        right_matcher = ximgproc::createRightMatcher(matcher);          // :10
+        // createDisparityWLSFilter(matcher) mutates the left matcher (:11)
+        matcher->setDisp12MaxDiff(1000000);
+        matcher->setSpeckleWindowSize(0);
+    }
+    // BGR 8UC3 rectified pair (full res) -> CV_32F disparity in px at half resolution
+    Mat computeDisparity(const Mat& left, const Mat& right) {
+        if (left.type != CV_8UC3 || right.type != CV_8UC3 || left.rows != right.rows ||
+            left.cols != right.cols || left.step != right.step)
+            throw Exception(SDR_ERR_TYPE, "computeDisparity expects two equal-size BGR images");
+        Mat out(left.rows / 2, left.cols / 2, CV_32FC1);
+        check(sdr_stereo_class_compute(matcher->handle(), right_matcher->handle(), left.data,
+                                       right.data, left.cols, left.rows, left.step,
+                                       out.ptr<float>(0), out.step / 4, nullptr, nullptr));
+        return out;
+    }
+    Mat computeDepth(const Mat& disparity) {  // stereo_disparity.cpp:76-80 (handleMissing=false)
+        Mat depth;
+        reprojectImageTo3D(disparity, depth, Q);
+        return depth;
+    }
+    const Ptr<StereoSGBM> get_matcher() const { return matcher; }
+
+private:
+    Ptr<StereoSGBM> matcher, right_matcher;
+    Mat Q;
+};
+
+}  // namespace sdr

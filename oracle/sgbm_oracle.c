@@ -736,8 +736,9 @@ void orc_reproject_f32(const float* disp, int width, int height, const double Q[
             double ia = 1. / h[3];
             float* o = xyz + ((size_t)y * width + x) * 3;
             for (int i = 0; i < 3; i++) {
-                float f = (float)h[i];
-                o[i] = (float)(f * ia);
+                /* volatile: GCC 11's SLP vectoriser drops this float narrowing at -O3 */
+                volatile float f = (float)h[i];
+                o[i] = (float)((double)f * ia);
             }
             if (fabs(d - minDisparity) <= FLT_EPSILON) o[2] = 10000.f;
         }

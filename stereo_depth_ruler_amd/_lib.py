@@ -63,6 +63,7 @@ SIGNATURES = [
     ("sdr_disp16_to_float_device", _i, [_vp, _vp, _sz, _vp]),
     ("sdr_bgr2gray_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
     ("sdr_resize_area_half_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
+    ("sdr_stereo_class_compute", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _sz, _vp, _vp]),
     ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),
     ("sdr_sgbm_enable_timing", _i, [_vp, _i]),
     ("sdr_sgbm_last_timing", _i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),

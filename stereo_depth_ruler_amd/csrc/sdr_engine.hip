@@ -134,6 +134,7 @@ struct sdr_sgbm {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     Buf planes, C, S, Caux, wta, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
+    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_f;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // per-kernel event pairs (timing level 2), harvested by sdr_sgbm_kernel_time
@@ -407,7 +408,8 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (Buf* b : {&h->planes, &h->C, &h->S, &h->Caux, &h->wta, &h->draw, &h->dlr, &h->dfin,
-                   &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz})
+                   &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
+                   &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_f})
         if (b->p) (void)hipFree(b->p);
     for (auto ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -628,6 +630,62 @@ int sdr_resize_area_half_device(const uint8_t* d_src, int W, int H, size_t strid
     if (dst_stride < (size_t)W / 2) return fail(SDR_ERR_ARG, "dst_stride < width/2");
     sdr::launch_area_half(d_src, W, H, stride, d_dst, dst_stride, F, (hipStream_t)stream);
     SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr_left,
+                             const uint8_t* bgr_right, int W, int H, size_t bgr_stride,
+                             float* out, size_t out_stride, int16_t* disp_left,
+                             int16_t* disp_right) {
+    if (!left || !bgr_left || !bgr_right || !out) return fail(SDR_ERR_ARG, "null argument");
+    if (W <= 0 || H <= 0 || bgr_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "bad size/stride");
+    if ((W & 1) || (H & 1)) return fail(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
+    if (right && right->device != left->device) return fail(SDR_ERR_ARG, "matchers on different devices");
+    const int w2 = W / 2, h2 = H / 2;
+    if (out_stride < (size_t)w2) return fail(SDR_ERR_ARG, "out_stride < width/2");
+    SDR_HIP(hipSetDevice(left->device));
+    hipStream_t st = left->stream;
+    const size_t px = (size_t)W * H, px2 = (size_t)w2 * h2;
+    int rc;
+    if ((rc = ensure(left->cls_bgr, 2 * px * 3))) return rc;
+    if ((rc = ensure(left->cls_gray, 2 * px))) return rc;
+    if ((rc = ensure(left->cls_small, 2 * px2))) return rc;
+    if ((rc = ensure(left->cls_dl, px2 * 2))) return rc;
+    if ((rc = ensure(left->cls_dr, px2 * 2))) return rc;
+    if ((rc = ensure(left->cls_f, px2 * 4))) return rc;
+    uint8_t* bgr = (uint8_t*)left->cls_bgr.p;
+    uint8_t* gray = (uint8_t*)left->cls_gray.p;
+    uint8_t* small = (uint8_t*)left->cls_small.p;
+    int16_t* dl = (int16_t*)left->cls_dl.p;
+    int16_t* dr = (int16_t*)left->cls_dr.p;
+    float* f = (float*)left->cls_f.p;
+    SDR_HIP(hipMemcpy2DAsync(bgr, (size_t)W * 3, bgr_left, bgr_stride, (size_t)W * 3, H, hipMemcpyHostToDevice, st));
+    SDR_HIP(hipMemcpy2DAsync(bgr + px * 3, (size_t)W * 3, bgr_right, bgr_stride, (size_t)W * 3, H,
+                             hipMemcpyHostToDevice, st));
+    // cvtColor(BGR2GRAY) x2, resize(0.5, INTER_AREA) x2 (stereo_disparity.cpp:19-24)
+    sdr::launch_bgr2gray(bgr, W, H, (size_t)W * 3, gray, W, 2, st);
+    sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
+    // matcher->compute(L, R) (stereo_disparity.cpp:27)
+    int16_t* fin = nullptr;
+    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, &fin))) return rc;
+    SDR_HIP(hipMemcpyAsync(dl, fin, px2 * 2, hipMemcpyDeviceToDevice, st));
+    if (right) {
+        // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
+        hipStream_t rs = right->stream;
+        right->stream = st;
+        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, &fin);
+        right->stream = rs;
+        if (rc) return rc;
+        SDR_HIP(hipMemcpyAsync(dr, fin, px2 * 2, hipMemcpyDeviceToDevice, st));
+    }
+    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34); WLS is not applied yet
+    sdr::launch_disp16_to_f32(dl, f, px2, st);
+    SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
+    if (disp_left)
+        SDR_HIP(hipMemcpyAsync(disp_left, dl, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_right && right)
+        SDR_HIP(hipMemcpyAsync(disp_right, dr, px2 * 2, hipMemcpyDeviceToHost, st));
+    SDR_HIP(hipStreamSynchronize(st));
     return SDR_OK;
 }
 

@@ -219,28 +219,28 @@ def createRightMatcher(matcher_left: StereoSGBM) -> StereoSGBM:
 def reprojectImageTo3D(disparity, Q, handleMissingValues=False):
     """cv::reprojectImageTo3D(disparity, _3dImage, Q, handleMissingValues) -> float32 (..., H, W, 3).
 
-    numpy float32 (H, W) -> numpy; torch CUDA float32 or int16 (1/16 px, fused convertTo)
-    (H, W) / (F, H, W) -> torch on the current stream."""
+    numpy float32/int16 (H, W) -> numpy; torch CUDA (H, W) / (F, H, W) -> torch on the current
+    stream.  As in OpenCV, int16 input is used as-is (no 1/16 scaling); see reproject_disp16 for
+    the fused convertTo(CV_32F, 1/16) + reproject of the reference (pcd_write.cpp:112-116)."""
     if _is_cuda(disparity):
         d = disparity
         squeeze = d.dim() == 2
         if squeeze:
             d = d.unsqueeze(0)
+        if d.dtype != torch.float32:
+            if d.dtype not in (torch.int16, torch.uint8, torch.int32):
+                raise SDRError(-5, "disparity must be float32, int16, int32 or uint8")
+            d = d.to(torch.float32)
         d = d.contiguous()
         f, h, w = d.shape
         out = torch.empty((f, h, w, 3), dtype=torch.float32, device=d.device)
-        st = _cstream(d.device.index)
-        if d.dtype == torch.int16:
-            check(lib().sdr_disp16_reproject_device(d.data_ptr(), w, h, w, _Q(Q),
-                                                    int(bool(handleMissingValues)), out.data_ptr(),
-                                                    w * 3, f, st))
-        elif d.dtype == torch.float32:
-            check(lib().sdr_reproject_device(d.data_ptr(), w, h, w, _Q(Q), int(bool(handleMissingValues)),
-                                             out.data_ptr(), w * 3, f, st))
-        else:
-            raise SDRError(-5, "disparity must be float32 or int16")
+        check(lib().sdr_reproject_device(d.data_ptr(), w, h, w, _Q(Q), int(bool(handleMissingValues)),
+                                         out.data_ptr(), w * 3, f, _cstream(d.device.index)))
         return out[0] if squeeze else out
-    d = np.ascontiguousarray(np.asarray(disparity, dtype=np.float32))
+    d = np.asarray(disparity)
+    if d.dtype not in (np.float32, np.int16, np.uint8, np.int32):
+        raise SDRError(-5, "disparity must be float32, int16, int32 or uint8")
+    d = np.ascontiguousarray(d, dtype=np.float32)
     if d.ndim != 2:
         raise SDRError(-1, "disparity must be 2-D")
     h, w = d.shape
@@ -248,6 +248,22 @@ def reprojectImageTo3D(disparity, Q, handleMissingValues=False):
     check(lib().sdr_reproject(d.ctypes.data, w, h, w, _Q(Q), int(bool(handleMissingValues)),
                               out.ctypes.data, w * 3))
     return out
+
+
+def reproject_disp16(disp16, Q, handleMissingValues=False):
+    """Fused disp.convertTo(CV_32F, 1/16) + reprojectImageTo3D on device (pcd_write.cpp:112-116)."""
+    if not _is_cuda(disp16) or disp16.dtype != torch.int16:
+        raise SDRError(-5, "reproject_disp16 expects a CUDA int16 tensor")
+    d = disp16
+    squeeze = d.dim() == 2
+    if squeeze:
+        d = d.unsqueeze(0)
+    d = d.contiguous()
+    f, h, w = d.shape
+    out = torch.empty((f, h, w, 3), dtype=torch.float32, device=d.device)
+    check(lib().sdr_disp16_reproject_device(d.data_ptr(), w, h, w, _Q(Q), int(bool(handleMissingValues)),
+                                            out.data_ptr(), w * 3, f, _cstream(d.device.index)))
+    return out[0] if squeeze else out
 
 
 def disparity_to_float(disp16):

@@ -1,0 +1,55 @@
+"""The reference's class surface, class StereoDisparity (stereo_vision/include/stereo_disparity.hpp:8-24,
+stereo_vision/src/stereo_disparity.cpp), on the HIP engine.
+
+computeDisparity(left, right): BGR 8UC3 full-res rectified pair -> CV_32F half-res disparity (px):
+cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left SGBM (3WAY, d=80) and right matcher -> /16,
+all on the GPU (sdr_stereo_class_compute).  The ximgproc WLS filter of stereo_disparity.cpp:31 is
+the next row of the build and is not applied yet: the left matcher's disparity is
+returned, with the matcher already mutated the way createDisparityWLSFilter mutates it
+(disp12MaxDiff = 1e6, speckleWindowSize = 0).
+computeDepth(disparity): reprojectImageTo3D(disparity, Q) (stereo_disparity.cpp:76-80), with the
+reference's quirk of a half-res disparity against the full-res Q kept as is.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import SDRError, check, lib
+from .sgbm import MODE_SGBM_3WAY, StereoSGBM, createRightMatcher, reprojectImageTo3D
+
+
+class StereoDisparity:
+    def __init__(self, Q_matrix, device: int = 0):
+        self.Q = np.asarray(Q_matrix, dtype=np.float64).reshape(4, 4).copy()
+        # stereo_disparity.cpp:5-9
+        self.matcher = StereoSGBM.create(0, 80, 5, 8 * 5 * 5 * 3, 32 * 5 * 5 * 3, 1, 63, 12, 200, 2,
+                                         MODE_SGBM_3WAY, device=device)
+        self.right_matcher = createRightMatcher(self.matcher)  # :10
+        # createDisparityWLSFilter(matcher) (:11) mutates the left matcher [ximgproc]
+        self.matcher.setDisp12MaxDiff(1000000)
+        self.matcher.setSpeckleWindowSize(0)
+        self.last_disp_left = None
+        self.last_disp_right = None
+
+    def computeDisparity(self, left, right):
+        left = np.ascontiguousarray(left, dtype=np.uint8)
+        right = np.ascontiguousarray(right, dtype=np.uint8)
+        if left.shape != right.shape or left.ndim != 3 or left.shape[2] != 3:
+            raise SDRError(-5, "computeDisparity expects two equal-size BGR (H, W, 3) images")
+        h, w, _ = left.shape
+        out = np.empty((h // 2, w // 2), np.float32)
+        dl = np.empty((h // 2, w // 2), np.int16)
+        dr = np.empty((h // 2, w // 2), np.int16)
+        check(lib().sdr_stereo_class_compute(self.matcher._h, self.right_matcher._h, left.ctypes.data,
+                                             right.ctypes.data, w, h, w * 3, out.ctypes.data, w // 2,
+                                             dl.ctypes.data, dr.ctypes.data))
+        self.last_disp_left, self.last_disp_right = dl, dr
+        return out
+
+    def computeDepth(self, disparity):
+        return reprojectImageTo3D(disparity, self.Q, False)
+
+    def get_matcher(self) -> StereoSGBM:
+        return self.matcher

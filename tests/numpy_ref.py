@@ -1,0 +1,125 @@
+"""Independent numpy restatements of single stages (vectorised, written from the published
+formulas, not from oracle/sgbm_oracle.c) used to pin the C oracle.  Test helpers only."""
+import numpy as np
+
+
+def prefilter_channels(img, ftzero):
+    """x-Sobel clipped to [0, 2*ftzero] and raw intensity; cols 0 / W-1 = ftzero (tab[0])."""
+    I = img.astype(np.int32)
+    H, W = I.shape
+    up = np.vstack([I[:1], I[:-1]])
+    dn = np.vstack([I[1:], I[-1:]])
+    sob = np.full((H, W), ftzero, np.int32)
+    raw = np.full((H, W), ftzero, np.int32)
+    g = 2 * (I[:, 2:] - I[:, :-2]) + (up[:, 2:] - up[:, :-2]) + (dn[:, 2:] - dn[:, :-2])
+    sob[:, 1:-1] = np.clip(g, -ftzero, ftzero) + ftzero
+    raw[:, 1:-1] = I[:, 1:-1]
+    return sob, raw
+
+
+def envelope(ch):
+    """(lo, hi) over the value and its two half-sample neighbours (truncating average)."""
+    W = ch.shape[1]
+    a = ch.copy()
+    b = ch.copy()
+    a[:, :-1] = (ch[:, :-1] + ch[:, 1:]) // 2
+    b[:, 1:] = (ch[:, 1:] + ch[:, :-1]) // 2
+    return np.minimum(np.minimum(a, b), ch), np.maximum(np.maximum(a, b), ch)
+
+
+def bt_cost_volume_rows(L, R, minD, D, ftzero):
+    """Pixel cost [H][W1][D] = BT(sobel) + (BT(raw) >> 2)."""
+    H, W = L.shape
+    maxD = minD + D
+    minX1, maxX1 = max(maxD, 0), W + min(minD, 0)
+    out = np.zeros((H, maxX1 - minX1, D), np.int32)
+    chans = []
+    for img in (L, R):
+        s, r = prefilter_channels(img, ftzero)
+        chans.append((s, r))
+    xs = np.arange(minX1, maxX1)
+    for c, scale in ((0, 0), (1, 2)):
+        u = chans[0][c]
+        v = chans[1][c]
+        u0, u1 = envelope(u)
+        v0, v1 = envelope(v)
+        for di, d in enumerate(range(minD, maxD)):
+            xr = xs - d
+            uu, uu0, uu1 = u[:, xs], u0[:, xs], u1[:, xs]
+            vv, vv0, vv1 = v[:, xr], v0[:, xr], v1[:, xr]
+            c0 = np.maximum(0, np.maximum(uu - vv1, vv0 - uu))
+            c1 = np.maximum(0, np.maximum(vv - uu1, uu0 - vv))
+            out[:, :, di] += np.minimum(c0, c1) >> scale
+    return out
+
+
+def cost_volume(L, R, minD, D, bs, P2, ftzero, hh=False):
+    """P2 + box(bs x bs) of the pixel costs with OpenCV's border rules (replicate inside
+    [0, W1) x [0, H); rows past H-1-SH2 repeat row H-1-SH2, or stay P2 for MODE_HH)."""
+    pix = bt_cost_volume_rows(L, R, minD, D, ftzero)
+    H, W1, _ = pix.shape
+    s = bs // 2
+    xi = np.clip(np.arange(W1)[:, None] + np.arange(-s, s + 1)[None, :], 0, W1 - 1)
+    hs = pix[:, xi, :].sum(2)
+    C = np.empty_like(hs)
+    ylim = max(H - 1 - s, 0)
+    for y in range(H):
+        if hh and y > 0 and y + s >= H:
+            C[y] = 0
+            continue
+        t = min(y, ylim)
+        rows = np.clip(np.arange(t - s, t + s + 1), 0, H - 1)
+        C[y] = hs[rows].sum(0)
+    return (C + P2).astype(np.int16)
+
+
+def speckle_filter(img, new_val, max_size, max_diff):
+    """Components by BFS over 4-neighbours joined when both != new_val and |diff| <= max_diff."""
+    H, W = img.shape
+    out = img.copy()
+    lab = -np.ones((H, W), np.int64)
+    n = 0
+    v = img.astype(np.int32)
+    for y0 in range(H):
+        for x0 in range(W):
+            if v[y0, x0] == new_val or lab[y0, x0] >= 0:
+                continue
+            stack = [(y0, x0)]
+            lab[y0, x0] = n
+            comp = []
+            while stack:
+                y, x = stack.pop()
+                comp.append((y, x))
+                for yy, xx in ((y + 1, x), (y - 1, x), (y, x + 1), (y, x - 1)):
+                    if 0 <= yy < H and 0 <= xx < W and lab[yy, xx] < 0 and v[yy, xx] != new_val \
+                            and abs(v[y, x] - v[yy, xx]) <= max_diff:
+                        lab[yy, xx] = n
+                        stack.append((yy, xx))
+            if len(comp) <= max_size:
+                for y, x in comp:
+                    out[y, x] = new_val
+            n += 1
+    return out
+
+
+def reproject(disp, Q, handle_missing=False):
+    """float64 Q @ (x, y, d, 1), sequential sums, Vec3f then * (1/w), Z=10000 at min(disp)."""
+    H, W = disp.shape
+    y, x = np.mgrid[0:H, 0:W].astype(np.float64)
+    d = disp.astype(np.float64)
+    h = []
+    for i in range(4):
+        s = np.zeros_like(d)
+        s = s + Q[i, 0] * x
+        s = s + Q[i, 1] * y
+        s = s + Q[i, 2] * d
+        s = s + Q[i, 3] * 1.0
+        h.append(s)
+    ia = 1.0 / h[3]
+    with np.errstate(all="ignore"):
+        out = np.stack([(h[i].astype(np.float32).astype(np.float64) * ia).astype(np.float32)
+                        for i in range(3)], -1)
+    if handle_missing:
+        m = float(disp.min())
+        out[..., 2][np.abs(d - m) <= np.finfo(np.float32).eps] = 10000.0
+    return out

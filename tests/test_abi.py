@@ -1,0 +1,102 @@
+"""C-ABI boundary checks that need no GPU: the HIP library loads, exports every function that
+include/sdr/sdr.h declares, the ctypes table matches the header, and host-only entry points
+(parameter defaults, createRightMatcher) behave like their OpenCV counterparts."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from stereo_depth_ruler_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sdr", "sdr.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(sdr_\w+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_loads():
+    assert _lib.lib().sdr_abi_version() == 1
+
+
+def test_every_declared_symbol_exported():
+    names = declared_functions()
+    assert len(names) >= 20, names
+    dll = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(dll, n), f"{n} declared in sdr.h but not exported"
+
+
+def test_ctypes_table_matches_header():
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == declared_functions()
+
+
+def test_params_struct_layout():
+    # 13 ints, in cv::StereoSGBM::create order, then nstripes / uniq_rule
+    assert ctypes.sizeof(_lib.SgbmParams) == 13 * 4
+    assert [f for f, _ in _lib.SgbmParams._fields_][:11] == [
+        "minDisparity", "numDisparities", "blockSize", "P1", "P2", "disp12MaxDiff", "preFilterCap",
+        "uniquenessRatio", "speckleWindowSize", "speckleRange", "mode"]
+
+
+def test_params_default_matches_opencv_create_defaults():
+    p = _lib.SgbmParams()
+    _lib.lib().sdr_sgbm_params_default(ctypes.byref(p))
+    assert (p.minDisparity, p.numDisparities, p.blockSize, p.P1, p.P2, p.disp12MaxDiff,
+            p.preFilterCap, p.uniquenessRatio, p.speckleWindowSize, p.speckleRange, p.mode) == (
+        0, 16, 3, 0, 0, 0, 0, 0, 0, 0, 0)
+    assert p.nstripes == 4
+
+
+def test_right_matcher_params():
+    """ximgproc createRightMatcher(StereoSGBM(0,80,5,600,2400,1,63,12,200,2,3WAY))."""
+    left = _lib.SgbmParams(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2, 4, 0)
+    r = _lib.SgbmParams()
+    _lib.lib().sdr_right_matcher_params(ctypes.byref(left), ctypes.byref(r))
+    assert (r.minDisparity, r.numDisparities, r.blockSize, r.P1, r.P2) == (-79, 80, 5, 600, 2400)
+    assert (r.uniquenessRatio, r.disp12MaxDiff, r.speckleWindowSize, r.mode, r.preFilterCap) == (
+        0, 1000000, 0, 2, 63)
+
+
+def test_scratch_bytes_is_pure_host():
+    p = _lib.SgbmParams(0, 128, 5, 600, 2400, 1, 63, 12, 200, 2, 0, 4, 0)
+    n = _lib.lib().sdr_sgbm_scratch_bytes(ctypes.byref(p), 1280, 720, 1)
+    cells = 720 * 1152 * 128
+    assert n >= 2 * cells * 2  # cost volume + path sums, int16
+    bad = _lib.SgbmParams(0, 100, 5, 600, 2400, 1, 63, 12, 200, 2, 0, 4, 0)
+    assert _lib.lib().sdr_sgbm_scratch_bytes(ctypes.byref(bad), 1280, 720, 1) == 0
+
+
+def test_create_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    p = _lib.SgbmParams(0, 16, 3, 0, 0, 0, 0, 0, 0, 0, 0, 4, 0)
+    h = ctypes.c_void_p()
+    rc = _lib.lib().sdr_sgbm_create(ctypes.byref(p), 0, ctypes.byref(h))
+    assert rc == -6 and not h.value
+    assert _lib.lib().sdr_last_error()
+
+
+def test_python_surface_raises_without_gpu():
+    import torch
+
+    import stereo_depth_ruler_amd as sdr
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(sdr.SDRError):
+        sdr.StereoSGBM.create(0, 16, 3)
+
+
+def test_null_arguments_rejected():
+    L = _lib.lib()
+    assert L.sdr_sgbm_compute(None, None, None, 8, 8, 1, 8, None, 8) == -1
+    assert L.sdr_reproject(None, 8, 8, 8, None, 0, None, 24) == -1
+    assert L.sdr_sgbm_set_params(None, None) == -1

@@ -83,8 +83,10 @@ int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out);
 int sdr_sgbm_destroy(sdr_sgbm* h);
 int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p);
 int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p);
-/* HIP stream (hipStream_t) the handle launches on; 0 = the handle's own stream. */
+/* HIP stream (hipStream_t) the handle launches on (NULL = the HIP null stream, e.g. torch's
+ * default stream); a new handle uses a stream of its own, restored by sdr_sgbm_reset_stream. */
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
+int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);
 
 /* Host-pointer compute (H2D, compute, D2H, synchronous): left/right 8-bit, `stride` bytes per

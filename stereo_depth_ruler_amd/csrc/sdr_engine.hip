@@ -433,7 +433,13 @@ int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p) {
 
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
-    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    h->stream = (hipStream_t)stream;  // NULL = the HIP null (legacy default) stream
+    return SDR_OK;
+}
+
+int sdr_sgbm_reset_stream(sdr_sgbm* h) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    h->stream = h->own_stream;
     return SDR_OK;
 }
 

@@ -119,7 +119,7 @@ def main():
     import stereo_depth_ruler_amd as sdr
     from stereo_depth_ruler_amd import synthetic as S
     from stereo_depth_ruler_amd.distributed import as_bytes
-    from stereo_depth_ruler_amd.sgbm import KERNEL_PATH_ADD
+    from stereo_depth_ruler_amd.sgbm import KERNEL_PATHS
 
     desc, W, H, args, batch, hm = CONFIGS[a.config]
     D, mode = args[1], args[10]
@@ -178,7 +178,7 @@ def main():
 
     roofline = None
     if not a.no_kernel_timing:
-        tot_ms, cnt = m.kernel_time(KERNEL_PATH_ADD, reset=False)
+        tot_ms, cnt = m.kernel_time(KERNEL_PATHS, reset=False)
         all_ms, all_cnt = m.kernel_time(-1, reset=True)
         m.enable_timing(0)
         w1 = W - max(args[0] + D, 0) + min(args[0], 0)

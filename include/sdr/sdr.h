@@ -145,9 +145,8 @@ size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, i
  * brackets every kernel launch; sdr_sgbm_kernel_time sums the launches of one SDR_KERNEL_* kind
  * (kind < 0: all) since the last reset. */
 enum {
-    SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATH_WRITE = 2,
-    SDR_KERNEL_PATH_ADD = 3, SDR_KERNEL_PATH_WTA = 4, SDR_KERNEL_LR = 5, SDR_KERNEL_MEDIAN = 6,
-    SDR_KERNEL_SPECKLE = 7, SDR_KERNEL_REPROJECT = 8
+    SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATHS = 2, SDR_KERNEL_WTA_LR = 3,
+    SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);
@@ -159,7 +158,7 @@ int sdr_selftest_wave_ops(int* failures4);
 
 /* Diagnostics: synchronously copy an internal buffer of the last compute to host memory.
  * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,
- * 2 = after the LR check, 3 = final (median + speckle), 4 = wta keys [F][H][W1] u32. */
+ * 2 = after the LR check, 3 = final (median + speckle), 4 = path costs L [P][F][H][W1][D] s16. */
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
 
 const char* sdr_last_error(void);

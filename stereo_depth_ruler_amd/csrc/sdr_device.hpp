@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 namespace sdr {
 
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -90,5 +93,27 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
 }
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// Compile-time unrolling of a step functor f(k, integral_constant<J>) over J = 0..N-1 (all steps)
+// or over the J with k0 + J <= klast (tail); J is the static ring slot of step k0 + J.
+template <typename F, int... J>
+__device__ __forceinline__ void unroll_rows(F& f, int k0, std::integer_sequence<int, J...>) {
+    (f(k0 + J, std::integral_constant<int, J>{}), ...);
+}
+template <typename F, int... J>
+__device__ __forceinline__ void unroll_rows_tail(F& f, int k0, int klast, std::integer_sequence<int, J...>) {
+    ((k0 + J <= klast ? f(k0 + J, std::integral_constant<int, J>{}) : void()), ...);
+}
+
+// trunc(n / d) for d >= 1 and |n / d| < 2^20 without a divide loop: float estimate, then one
+// exact integer correction step (the subpixel quotients are in [-9, 9]).
+__device__ __forceinline__ int div_trunc_small(int n, int d) {
+    const int an = abs(n);
+    int q = (int)((float)an * __builtin_amdgcn_rcpf((float)d));
+    const int r = an - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return n < 0 ? -q : q;
+}
 
 }  // namespace sdr

@@ -77,7 +77,7 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     e->speckle_ws = p.speckleWindowSize;
     e->speckle_diff = 16 * p.speckleRange;
     e->blockSize = p.blockSize;
-    if (g.SH2 > 10 || g.SW2 > 10) return fail(SDR_ERR_ARG, "blockSize > 21 is not supported");
+    if (g.SH2 > 5 || g.SW2 > 5) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
     if (g.P2 > 16383) return fail(SDR_ERR_ARG, "P2 too large for int16 path costs");
     return SDR_OK;
 }
@@ -133,7 +133,7 @@ struct sdr_sgbm {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    Buf planes, C, S, Caux, wta, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
+    Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_f;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -168,11 +168,8 @@ struct KTimer {
 };
 }  // namespace
 
-static int choose_tx(const sdr::Geometry& g) {
-    int TX = g.D <= 128 ? 32 : 16;
-    while (TX > 4 && sdr::cost_lds_bytes(g, TX) > 64 * 1024) TX /= 2;
-    return TX;
-}
+
+static int npaths_of(int mode);
 
 static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
     const sdr::Geometry& g = e.g;
@@ -185,11 +182,17 @@ static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
         aux = (size_t)st->size() * amax * std::max(g.W1, 0) * g.D * 2;
     }
     const size_t px = (size_t)g.W * g.H;
-    return (size_t)F * (2 * px * 8 + cells * 2 * 2 + aux + (size_t)g.H * std::max(g.W1, 0) * 4 +
-                        px * 2 * 3 + px * 4 * 2);
+    return (size_t)F * (6 * px * 8 + cells * 2 * (1 + npaths_of(e.mode)) + aux + px * 2 * 3 +
+                        px * 4 * 2);
 }
 
+static int npaths_of(int mode) { return mode == SDR_MODE_HH ? 8 : mode == SDR_MODE_SGBM ? 5 : 3; }
+
 // Enqueues the full compute for F frames whose inputs are already on the device.
+//   prefilter -> cost volume (+ 3WAY stripe-start rows) -> all path directions in one launch,
+//   each into its own L buffer -> WTA/uniqueness/subpixel/disp2/LR per row -> median3 -> speckle
+// Per cell this moves 2 (C write) + 4P (paths: C read + L write) + 2P (WTA: L reads) bytes,
+// the canonical 2 + 6P of SURVEY.md 8(d).
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t** final_disp) {
     Eff e;
@@ -207,19 +210,22 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     if (g.W1 <= g.SW2) return fail(SDR_ERR_SIZE, "image too narrow for numDisparities/blockSize");
     if (W > 8192) return fail(SDR_ERR_SIZE, "width > 8192 is not supported");
+    if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
 
     const size_t cells = (size_t)H * g.W1 * g.D;
+    const int P = npaths_of(e.mode);
     std::vector<Stripe> stripes;
     if (e.mode == SDR_MODE_SGBM_3WAY) stripes_of(e, &stripes);
+    if (stripes.size() + 2 > (size_t)sdr::kMaxPathDirs) return fail(SDR_ERR_ARG, "too many 3WAY stripes");
     int amax = 0;
     for (auto& s : stripes) amax = std::max(amax, s.aux_rows);
     const size_t aux_fstride = (size_t)stripes.size() * amax * g.W1 * g.D;
 
-    if ((rc = ensure(h->planes, F * 2 * px * 8))) return rc;
+    if ((rc = ensure(h->planesL, F * 3 * px * 8))) return rc;
+    if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
     if ((rc = ensure(h->C, F * cells * 2))) return rc;
-    if ((rc = ensure(h->S, F * cells * 2))) return rc;
+    if ((rc = ensure(h->Lr, (size_t)P * F * cells * 2))) return rc;
     if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
-    if ((rc = ensure(h->wta, F * (size_t)H * g.W1 * 4))) return rc;
     if ((rc = ensure(h->draw, F * px * 2))) return rc;
     if ((rc = ensure(h->dlr, F * px * 2))) return rc;
     if (e.speckle_ws > 0) {
@@ -228,20 +234,20 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
 
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[0], st));
-    uint64_t* planes = (uint64_t*)h->planes.p;
     int16_t* C = (int16_t*)h->C.p;
-    int16_t* S = (int16_t*)h->S.p;
     int16_t* Caux = (int16_t*)h->Caux.p;
-    uint32_t* wta = (uint32_t*)h->wta.p;
+    int16_t* Lr = (int16_t*)h->Lr.p;  // [P][F][H][W1][D]
     int16_t* draw = (int16_t*)h->draw.p;
     int16_t* dlr = (int16_t*)h->dlr.p;
 
-    sdr::launch_fill_s16(draw, (int16_t)e.invalid, F * px, st);
-    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, planes, st); }
+    sdr::Planes pl;
+    pl.L = (uint64_t*)h->planesL.p;
+    pl.R = (uint64_t*)h->planesR.p;
+    pl.fstrideL = pl.fstrideR = 3 * px;
+    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st); }
 
     sdr::CostArgs ca{};
-    ca.planes = planes;
-    ca.planes_fstride = 2 * px;
+    ca.pl = pl;
     ca.out = C;
     ca.out_fstride = cells;
     ca.out_row0 = 0;
@@ -250,7 +256,6 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     ca.s0 = 0;
     ca.ylim = std::max(H - 1 - g.SH2, 0);
     ca.hh_bottom = e.mode == SDR_MODE_HH;
-    ca.TX = choose_tx(g);
     ca.TY = 32;
     { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
     for (size_t s = 0; s < stripes.size(); s++) {
@@ -271,71 +276,68 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));
 
-    sdr::PathArgs pa{};
-    pa.C = C;
-    pa.S = S;
-    pa.cs_fstride = cells;
-    pa.disp_raw = draw;
-    pa.wta = wta;
-    pa.disp_fstride = px;
-    pa.wta_fstride = (size_t)H * g.W1;
-    pa.uniq = e.uniq;
-    pa.uniq_simd = e.uniq_simd;
-    pa.ybeg = 0;
-    pa.yend = H;
-    pa.write_from = 0;
-    const int nE = H, nS = g.W1, nD = g.W1 + H - 1;
-    auto run = [&](int dir, int smode, int nch) {
-        sdr::PathArgs q = pa;
-        q.dir = dir;
-        KTimer kt(h, SDR_KERNEL_PATH_WRITE + smode);
-        sdr::launch_path(g, q, smode, nch, F, st);
+    sdr::PathLaunch pls{};
+    pls.C = C;
+    pls.cs_fstride = cells;
+    pls.aux_fstride = aux_fstride;
+    pls.ndirs = 0;
+    int nbuf = 0;
+    auto add_dir = [&](int dir, int nch, int16_t* out) {
+        sdr::PathDir d{};
+        d.dir = dir;
+        d.nchains = nch;
+        d.ybeg = 0;
+        d.yend = H;
+        d.write_from = 0;
+        d.out = out;
+        pls.d[pls.ndirs++] = d;
     };
-    if (e.mode == SDR_MODE_SGBM) {
-        run(sdr::DIR_E, sdr::S_WRITE, nE);
-        run(sdr::DIR_SE, sdr::S_ADD, nD);
-        run(sdr::DIR_S, sdr::S_ADD, nS);
-        run(sdr::DIR_SW, sdr::S_ADD, nD);
-        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
-    } else if (e.mode == SDR_MODE_HH) {
-        run(sdr::DIR_E, sdr::S_WRITE, nE);
-        run(sdr::DIR_SE, sdr::S_ADD, nD);
-        run(sdr::DIR_S, sdr::S_ADD, nS);
-        run(sdr::DIR_SW, sdr::S_ADD, nD);
-        run(sdr::DIR_NE, sdr::S_ADD, nD);
-        run(sdr::DIR_N, sdr::S_ADD, nS);
-        run(sdr::DIR_NW, sdr::S_ADD, nD);
-        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
-    } else {
-        run(sdr::DIR_E, sdr::S_WRITE, nE);
+    auto buf = [&]() { return Lr + (size_t)(nbuf++) * F * cells; };
+    const int nE = H, nS = g.W1, nD = g.W1 + H - 1;
+    // longest chains first: the E/W rows (W1 steps) are dispatched before the shorter ones
+    add_dir(sdr::DIR_E, nE, buf());
+    add_dir(sdr::DIR_W, nE, buf());
+    if (e.mode == SDR_MODE_SGBM_3WAY) {
+        int16_t* out = buf();
         for (size_t s = 0; s < stripes.size(); s++) {
             const Stripe& sp = stripes[s];
-            sdr::PathArgs q = pa;
-            q.dir = sdr::DIR_S;
-            q.ybeg = sp.s0;
-            q.yend = sp.end;
-            q.write_from = sp.out0;
+            add_dir(sdr::DIR_S, nS, out);
+            sdr::PathDir& d = pls.d[pls.ndirs - 1];
+            d.ybeg = sp.s0;
+            d.yend = sp.end;
+            d.write_from = sp.out0;
             if (sp.aux_rows) {
-                q.Caux = Caux + s * (size_t)amax * g.W1 * g.D;
-                q.aux_fstride = aux_fstride;
-                q.aux_row0 = sp.s0;
-                q.aux_rows = sp.aux_rows;
+                d.Caux = Caux + s * (size_t)amax * g.W1 * g.D;
+                d.aux_row0 = sp.s0;
+                d.aux_rows = sp.aux_rows;
             }
-            KTimer kt(h, SDR_KERNEL_PATH_ADD);
-            sdr::launch_path(g, q, sdr::S_ADD, nS, F, st);
         }
-        run(sdr::DIR_W, sdr::S_ADD_WTA, nE);
+    } else {
+        add_dir(sdr::DIR_S, nS, buf());
+        if (e.mode == SDR_MODE_HH) add_dir(sdr::DIR_N, nS, buf());
+        add_dir(sdr::DIR_SE, nD, buf());
+        add_dir(sdr::DIR_SW, nD, buf());
+        if (e.mode == SDR_MODE_HH) {
+            add_dir(sdr::DIR_NE, nD, buf());
+            add_dir(sdr::DIR_NW, nD, buf());
+        }
     }
+    pls.prefix[0] = 0;
+    for (int i = 0; i < pls.ndirs; i++) pls.prefix[i + 1] = pls.prefix[i] + pls.d[i].nchains;
+    { KTimer kt(h, SDR_KERNEL_PATHS); sdr::launch_paths(g, pls, F, st); }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
-    sdr::LrArgs la{};
-    la.disp_raw = draw;
-    la.wta = wta;
-    la.out = dlr;
-    la.disp_fstride = px;
-    la.wta_fstride = (size_t)H * g.W1;
-    la.disp12MaxDiff = e.disp12MaxDiff;
-    { KTimer kt(h, SDR_KERNEL_LR); sdr::launch_lr(g, la, F, st); }
+    sdr::WtaArgs wa{};
+    for (int p = 0; p < P; p++) wa.L[p] = Lr + (size_t)p * F * cells;
+    wa.npaths = P;
+    wa.cs_fstride = cells;
+    wa.disp_raw = draw;
+    wa.disp_lr = dlr;
+    wa.disp_fstride = px;
+    wa.uniq = e.uniq;
+    wa.uniq_simd = e.uniq_simd;
+    wa.disp12MaxDiff = e.disp12MaxDiff;
+    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_wta_lr(g, wa, F, st); }
     { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, dfin, W, H, F, st); }
     if (e.speckle_ws > 0) {
         KTimer kt(h, SDR_KERNEL_SPECKLE);
@@ -407,7 +409,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (Buf* b : {&h->planes, &h->C, &h->S, &h->Caux, &h->wta, &h->draw, &h->dlr, &h->dfin,
+    for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_f})
         if (b->p) (void)hipFree(b->p);
@@ -718,7 +720,7 @@ int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int*
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) {
     if (!h || !dst) return fail(SDR_ERR_ARG, "null argument");
     const Buf* b = stage == 0 ? &h->C : stage == 1 ? &h->draw : stage == 2 ? &h->dlr
-                 : stage == 3 ? &h->dfin : stage == 4 ? &h->wta : nullptr;
+                 : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : nullptr;
     if (!b) return fail(SDR_ERR_ARG, "bad stage");
     if (!b->p || bytes > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));

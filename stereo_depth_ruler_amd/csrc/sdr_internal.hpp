@@ -1,4 +1,4 @@
-// sdr_internal.hpp -- launchers shared between sdr_kernels.hip and sdr_engine.hip.
+// sdr_internal.hpp -- launchers shared by the kernel files and sdr_engine.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -6,20 +6,17 @@
 
 namespace sdr {
 
-// Scanline directions of the path recurrence.  dx/dy = step between
-// consecutive pixels of one chain.
+// Scanline directions of the path recurrence.
 enum Dir : int {
     DIR_E = 0,   // -> (x ascending)        OpenCV dir 0, pass 1
     DIR_W = 1,   // <- (x descending)       OpenCV dir 4 (SGBM/3WAY), dir 0 pass 2 (HH)
-    DIR_S = 2,   // top -> bottom           dir 2 pass 1
+    DIR_S = 2,   // top -> bottom           dir 2 pass 1 (3WAY: per stripe)
     DIR_N = 3,   // bottom -> top           dir 2 pass 2 (HH)
     DIR_SE = 4,  // (x-1,y-1) -> (x,y)      dir 1 pass 1
     DIR_SW = 5,  // (x+1,y-1) -> (x,y)      dir 3 pass 1
     DIR_NE = 6,  // (x-1,y+1) -> (x,y)      dir 1 pass 2 (HH)
     DIR_NW = 7,  // (x+1,y+1) -> (x,y)      dir 3 pass 2 (HH)
 };
-
-enum SMode : int { S_WRITE = 0, S_ADD = 1, S_ADD_WTA = 2 };
 
 struct Geometry {
     int W, H;           // image size
@@ -29,9 +26,15 @@ struct Geometry {
     int P1, P2;
 };
 
+// ---- prefilter / cost volume (sdr_cost.hip) ----
+struct Planes {
+    uint64_t* L;        // [F][H][W] bytes {sob, sob_lo, sob_hi, raw, raw_lo, raw_hi, 0, 0}
+    uint64_t* R;        // [F][3][H][W] int16 pairs (q(x) | q(x-1) << 16): {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
+    size_t fstrideL, fstrideR;  // elements per frame
+};
+
 struct CostArgs {
-    const uint64_t* planes;  // [F][2][H][W] BT planes (left, right)
-    size_t planes_fstride;   // elements per frame
+    Planes pl;
     int16_t* out;            // cost rows
     size_t out_fstride;      // elements per frame
     int out_row0;            // row index of out's first row
@@ -39,43 +42,48 @@ struct CostArgs {
     int s0;                  // chain/box start row (box clamp)
     int ylim;                // rows > ylim repeat row ylim (running sum stops updating)
     int hh_bottom;           // MODE_HH: rows y>0 with y+SH2>=H keep the initial P2
-    int TX;                  // tile width (matched columns)
     int TY;                  // tile height (output rows)
 };
 
-struct PathArgs {
-    const int16_t* C;        // [F][H][W1][D]
-    int16_t* S;              // [F][H][W1][D]
-    const int16_t* Caux;     // 3WAY stripe-start rows [F][aux_rows][W1][D] or null
-    size_t cs_fstride;       // elements per frame of C/S
-    size_t aux_fstride;
-    int aux_row0, aux_rows;
+// ---- path aggregation (sdr_paths.hip) ----
+constexpr int kMaxPathDirs = 24;
+constexpr int kMaxPaths = 8;
+
+struct PathDir {
     int dir;
-    int ybeg, yend;          // vertical chain row range (DIR_S): [ybeg, yend)
-    int write_from;          // DIR_S: first row whose S is written (3WAY stripe output start)
-    // WTA (S_ADD_WTA)
-    int16_t* disp_raw;       // [F][H][W] int16 (matched columns written)
-    uint32_t* wta;           // [F][H][W1] (minS << 16 | best) or 0xffffffff
-    size_t disp_fstride, wta_fstride;
-    int uniq, uniq_simd;
+    int nchains;
+    int ybeg, yend, write_from;  // DIR_S chain rows (3WAY stripes); others: 0, H, 0
+    int aux_row0, aux_rows;      // DIR_S chains read stripe-local cost rows for their first rows
+    const int16_t* Caux;         // [F][aux_rows][W1][D] or null
+    int16_t* out;                // L of this direction [F][H][W1][D]
 };
 
-struct LrArgs {
-    const int16_t* disp_raw; // [F][H][W]
-    const uint32_t* wta;     // [F][H][W1]
-    int16_t* out;            // [F][H][W]
-    size_t disp_fstride, wta_fstride;
-    int disp12MaxDiff;
+struct PathLaunch {
+    const int16_t* C;
+    size_t cs_fstride;   // elements per frame (C and every L buffer)
+    size_t aux_fstride;
+    int ndirs;
+    int prefix[kMaxPathDirs + 1];  // chain prefix sums
+    PathDir d[kMaxPathDirs];
+};
+
+struct WtaArgs {
+    const int16_t* L[kMaxPaths];  // per-direction path costs [F][H][W1][D]
+    int npaths;
+    size_t cs_fstride;
+    int16_t* disp_raw;   // WTA disparity before the LR check [F][H][W]
+    int16_t* disp_lr;    // after the LR check [F][H][W]
+    size_t disp_fstride;
+    int uniq, uniq_simd, disp12MaxDiff;
 };
 
 void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st);
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
-                      int H, int F, int ftzero, uint64_t* planes, hipStream_t st);
-int cost_lds_bytes(const Geometry& g, int TX);
+                      int H, int F, int ftzero, const Planes& pl, hipStream_t st);
+bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
-void launch_path(const Geometry& g, const PathArgs& a, int smode, int nchains, int F,
-                 hipStream_t st);
-void launch_lr(const Geometry& g, const LrArgs& a, int F, hipStream_t st);
+void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
+void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
 void launch_speckle(int16_t* img, int W, int H, int F, int newVal, int maxSize, int maxDiff,
                     int* labels, int* sizes, hipStream_t st);

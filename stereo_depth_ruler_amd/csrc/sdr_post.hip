@@ -1,0 +1,424 @@
+// sdr_post.hip -- post-WTA stages: A.10 median 3x3, A.11 speckle filter (connected components),
+// per-frame minimum, A.12 reprojectImageTo3D, convertTo(1/16), A.13 class-path pre-steps
+// (BGR2GRAY, INTER_AREA 0.5x) and a device self-test of the cross-lane primitives.
+#include "sdr_device.hpp"
+#include "sdr_internal.hpp"
+
+#include <float.h>
+
+namespace sdr {
+
+// ------------------------------------------------------------------------------------------
+// A.10 medianBlur 3x3, replicate border (Devillard's 19-exchange median-of-9 network)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src,
+                                                 int16_t* __restrict__ dst, int W, int H) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const size_t fo = (size_t)blockIdx.z * W * H;
+    if (x >= W || y >= H) return;
+    int p[9];
+    const int xs[3] = {max(x - 1, 0), x, min(x + 1, W - 1)};
+    const int ys[3] = {max(y - 1, 0), y, min(y + 1, H - 1)};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) p[i * 3 + j] = src[fo + (size_t)ys[i] * W + xs[j]];
+#define SDR_S(a, b) { int t_ = min(p[a], p[b]); p[b] = max(p[a], p[b]); p[a] = t_; }
+    SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 1) SDR_S(3, 4) SDR_S(6, 7)
+    SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 3) SDR_S(5, 8) SDR_S(4, 7)
+    SDR_S(3, 6) SDR_S(1, 4) SDR_S(2, 5) SDR_S(4, 7) SDR_S(4, 2) SDR_S(6, 4)
+    SDR_S(4, 2)
+#undef SDR_S
+    dst[fo + (size_t)y * W + x] = (int16_t)p[4];
+}
+
+void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st) {
+    dim3 grid((W + 63) / 64, (H + 3) / 4, F);
+    hipLaunchKernelGGL(k_median3, grid, dim3(256), 0, st, src, dst, W, H);
+}
+
+// ------------------------------------------------------------------------------------------
+// A.11 filterSpeckles as connected-component labelling: 4-neighbours p,q are joined iff
+// neither equals newVal and |v(p)-v(q)| <= maxDiff; components of <= maxSize pixels are set to
+// newVal.  Lock-free union-find with atomicMin (Playne & Hawick 2018), then flatten, count,
+// apply.  The flood fill of OpenCV and CCL give identical components (the join relation is
+// symmetric and evaluated on the unmodified image).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int uf_load(int* P, int i) {
+    return __hip_atomic_load(&P[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int uf_find(int* P, int x) {
+    int p = uf_load(P, x);
+    while (p != x) {
+        x = p;
+        p = uf_load(P, x);
+    }
+    return x;
+}
+__device__ __forceinline__ void uf_unite(int* P, int a, int b) {
+    for (;;) {
+        a = uf_find(P, a);
+        b = uf_find(P, b);
+        if (a == b) return;
+        if (a < b) {
+            int old = atomicMin(&P[b], a);
+            if (old == b) return;
+            b = old;
+        } else {
+            int old = atomicMin(&P[a], b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+// Tile-local pass: 32x32 tile in LDS, union-find with LDS atomics, roots written as global
+// pixel indices.  Then only tile borders are merged with global atomics.
+constexpr int kCT = 32;
+
+__device__ __forceinline__ int lds_find(int* lab, int x) {
+    int p = __hip_atomic_load(&lab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(&lab[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return x;
+}
+__device__ __forceinline__ void lds_unite(int* lab, int a, int b) {
+    for (;;) {
+        a = lds_find(lab, a);
+        b = lds_find(lab, b);
+        if (a == b) return;
+        if (a < b) {
+            int old = atomicMin(&lab[b], a);
+            if (old == b) return;
+            b = old;
+        } else {
+            int old = atomicMin(&lab[a], b);
+            if (old == a) return;
+            a = old;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ccl_local(const int16_t* img, int* P, int* sizes, int W,
+                                                   int H, int newVal, int maxDiff) {
+    __shared__ int16_t v[kCT * kCT];
+    __shared__ int lab[kCT * kCT];
+    const int tx0 = blockIdx.x * kCT, ty0 = blockIdx.y * kCT;
+    const size_t fo = (size_t)blockIdx.z * W * H;
+    const int16_t* I = img + fo;
+    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
+        const int gx = tx0 + (i & (kCT - 1)), gy = ty0 + (i >> 5);
+        int val = newVal;
+        if (gx < W && gy < H) val = I[(size_t)gy * W + gx];
+        v[i] = (int16_t)val;
+        lab[i] = val != newVal ? i : -1;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
+        if (lab[i] < 0) continue;
+        const int lx = i & (kCT - 1), ly = i >> 5;
+        const int val = v[i];
+        if (lx + 1 < kCT && lab[i + 1] >= 0 && abs(val - v[i + 1]) <= maxDiff) lds_unite(lab, i, i + 1);
+        if (ly + 1 < kCT && lab[i + kCT] >= 0 && abs(val - v[i + kCT]) <= maxDiff) lds_unite(lab, i, i + kCT);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
+        const int gx = tx0 + (i & (kCT - 1)), gy = ty0 + (i >> 5);
+        if (gx >= W || gy >= H) continue;
+        const size_t g = (size_t)gy * W + gx;
+        int r = -1;
+        if (lab[i] >= 0) {
+            const int lr = lds_find(lab, i);
+            r = (ty0 + (lr >> 5)) * W + tx0 + (lr & (kCT - 1));
+        }
+        P[fo + g] = r;
+        sizes[fo + g] = 0;
+    }
+}
+
+// merge across tile borders: vertical borders (x = 32k-1 | 32k) and horizontal ones
+__global__ void k_ccl_merge(const int16_t* img, int* P, int W, int H, int newVal, int maxDiff) {
+    const size_t fo = (size_t)blockIdx.y * W * H;
+    const int16_t* I = img + fo;
+    int* Pf = P + fo;
+    const int nvx = (W - 1) / kCT, nhy = (H - 1) / kCT;
+    const int nv = nvx * H, nh = nhy * W;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nv + nh; t += gridDim.x * blockDim.x) {
+        int a, b;
+        if (t < nv) {
+            const int y = t / nvx, x = (t - y * nvx + 1) * kCT - 1;
+            a = y * W + x;
+            b = a + 1;
+        } else {
+            const int u = t - nv;
+            const int yb = u / W, x = u - yb * W;
+            const int y = (yb + 1) * kCT - 1;
+            a = y * W + x;
+            b = a + W;
+        }
+        const int va = I[a], vb = I[b];
+        if (va != newVal && vb != newVal && abs(va - vb) <= maxDiff) uf_unite(Pf, a, b);
+    }
+}
+
+// flatten to roots and count component sizes with one atomic per (wave, root)
+__global__ void k_ccl_count(int* P, int* sizes, int n) {
+    const size_t fo = (size_t)blockIdx.y * n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int r = -1;
+    if (i < n) {
+        r = P[fo + i];
+        if (r >= 0) {
+            r = uf_find(P + fo, r);
+            P[fo + i] = r;
+        }
+    }
+    unsigned long long pend = __ballot(r >= 0);
+    const int lane = threadIdx.x & 63;
+    while (pend) {
+        const int src = __ffsll((long long)pend) - 1;
+        const int lr = __shfl(r, src);
+        const unsigned long long m = __ballot(r == lr) & pend;
+        if (lane == src) atomicAdd(&sizes[fo + lr], __popcll(m));
+        pend &= ~m;
+    }
+}
+
+__global__ void k_ccl_apply(int16_t* img, const int* P, const int* sizes, int n, int newVal,
+                            int maxSize) {
+    const size_t fo = (size_t)blockIdx.y * n;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = P[fo + i];
+    if (r >= 0 && sizes[fo + r] <= maxSize) img[fo + i] = (int16_t)newVal;
+}
+
+void launch_speckle(int16_t* img, int W, int H, int F, int newVal, int maxSize, int maxDiff,
+                    int* labels, int* sizes, hipStream_t st) {
+    const int n = W * H;
+    hipLaunchKernelGGL(k_ccl_local, dim3((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, F), dim3(256), 0,
+                       st, img, labels, sizes, W, H, newVal, maxDiff);
+    const int nb = ((W - 1) / kCT) * H + ((H - 1) / kCT) * W;
+    if (nb > 0)
+        hipLaunchKernelGGL(k_ccl_merge, dim3((unsigned)min((nb + 255) / 256, 1024), F), dim3(256), 0,
+                           st, img, labels, W, H, newVal, maxDiff);
+    hipLaunchKernelGGL(k_ccl_count, dim3((n + 255) / 256, F), dim3(256), 0, st, labels, sizes, n);
+    hipLaunchKernelGGL(k_ccl_apply, dim3((n + 255) / 256, F), dim3(256), 0, st, img, labels, sizes, n,
+                       newVal, maxSize);
+}
+
+// ------------------------------------------------------------------------------------------
+// per-frame minimum (reprojectImageTo3D handleMissingValues needs min(disp))
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_min_s16(const int16_t* img, size_t n, size_t fstride, int* out) {
+    __shared__ int wm[4];
+    const int16_t* I = img + (size_t)blockIdx.y * fstride;
+    int m = 32767;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        m = min(m, (int)I[i]);
+    m = (int)wave_min_u32((uint32_t)(m + 32768)) - 32768;
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMin(&out[blockIdx.y], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
+}
+
+__global__ void k_init_i32(int* p, int v, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
+                    hipStream_t st) {
+    hipLaunchKernelGGL(k_init_i32, dim3((F + 255) / 256), dim3(256), 0, st, out_min, 32767, F);
+    dim3 grid((unsigned)min((n_per_frame + 1023) / 1024, (size_t)128), F);
+    hipLaunchKernelGGL(k_min_s16, grid, dim3(256), 0, st, img, n_per_frame, fstride, out_min);
+}
+
+// ------------------------------------------------------------------------------------------
+// A.12 reprojectImageTo3D: double math, sequential sums from 0, no contraction, Vec3f then
+// *(1.0/h3) rounded to float; handleMissing: Z = 10000 where |d - min(disp)| <= FLT_EPSILON.
+// ------------------------------------------------------------------------------------------
+struct Q16 {
+    double q[16];
+};
+
+__device__ __forceinline__ void reproject_px(const Q16& Q, int x, int y, double d, double mind,
+                                             int hm, float* o) {
+#pragma clang fp contract(off)
+    const double v0 = (double)x, v1 = (double)y;
+    double h[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double s = 0.0;
+        s += Q.q[i * 4 + 0] * v0;
+        s += Q.q[i * 4 + 1] * v1;
+        s += Q.q[i * 4 + 2] * d;
+        s += Q.q[i * 4 + 3] * 1.0;
+        h[i] = s;
+    }
+    const double ia = 1.0 / h[3];
+    const float X = (float)((double)(float)h[0] * ia);
+    const float Y = (float)((double)(float)h[1] * ia);
+    float Z = (float)((double)(float)h[2] * ia);
+    if (hm && fabs(d - mind) <= (double)FLT_EPSILON) Z = 10000.f;
+    o[0] = X;
+    o[1] = Y;
+    o[2] = Z;
+}
+
+__global__ __launch_bounds__(256) void k_reproject_s16(const int16_t* disp, int W, int H,
+                                                       size_t dstride, size_t dfstride, Q16 Q,
+                                                       int hm, const int* mins, float* xyz,
+                                                       size_t xstride, size_t xfstride) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= W) return;
+    const int v = disp[(size_t)f * dfstride + (size_t)y * dstride + x];
+    const double d = (double)((float)v * 0.0625f);
+    const double mind = hm ? (double)((float)mins[f] * 0.0625f) : (double)FLT_MAX;
+    reproject_px(Q, x, y, d, mind, hm, xyz + (size_t)f * xfstride + (size_t)y * xstride + 3 * (size_t)x);
+}
+
+__device__ __forceinline__ int f2ord(float f) {
+    int i = __float_as_int(f);
+    return i < 0 ? i ^ 0x7fffffff : i;
+}
+__device__ __forceinline__ float ord2f(int i) {
+    return __int_as_float(i < 0 ? i ^ 0x7fffffff : i);
+}
+
+__global__ void k_min_f32(const float* disp, int W, int H, size_t dstride, size_t dfstride, int* out) {
+    const float* I = disp + (size_t)blockIdx.y * dfstride;
+    int m = 0x7fffffff;
+    const size_t n = (size_t)W * H;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        float v = I[(i / W) * dstride + (i % W)];
+        if (v == v) m = min(m, f2ord(v));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMin(&out[blockIdx.y], m);
+}
+
+__global__ __launch_bounds__(256) void k_reproject_f32(const float* disp, int W, int H,
+                                                       size_t dstride, size_t dfstride, Q16 Q,
+                                                       int hm, const int* minbits, float* xyz,
+                                                       size_t xstride, size_t xfstride) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= W) return;
+    const double d = (double)disp[(size_t)f * dfstride + (size_t)y * dstride + x];
+    const double mind = hm ? (double)ord2f(minbits[f]) : (double)FLT_MAX;
+    reproject_px(Q, x, y, d, mind, hm, xyz + (size_t)f * xfstride + (size_t)y * xstride + 3 * (size_t)x);
+}
+
+void launch_reproject_s16(const int16_t* disp, int W, int H, size_t dstride, size_t dfstride,
+                          const double* Q, int hm, const int* mins, float* xyz, size_t xstride,
+                          size_t xfstride, int F, hipStream_t st) {
+    Q16 q;
+    for (int i = 0; i < 16; i++) q.q[i] = Q[i];
+    hipLaunchKernelGGL(k_reproject_s16, dim3((W + 255) / 256, H, F), dim3(256), 0, st, disp, W, H,
+                       dstride, dfstride, q, hm, mins, xyz, xstride, xfstride);
+}
+
+void launch_reproject_f32(const float* disp, int W, int H, size_t dstride, size_t dfstride,
+                          const double* Q, int hm, int* minbits, float* xyz, size_t xstride,
+                          size_t xfstride, int F, hipStream_t st) {
+    Q16 q;
+    for (int i = 0; i < 16; i++) q.q[i] = Q[i];
+    if (hm) {
+        hipLaunchKernelGGL(k_init_i32, dim3((F + 255) / 256), dim3(256), 0, st, minbits, 0x7fffffff, F);
+        hipLaunchKernelGGL(k_min_f32, dim3(256, F), dim3(256), 0, st, disp, W, H, dstride, dfstride, minbits);
+    }
+    hipLaunchKernelGGL(k_reproject_f32, dim3((W + 255) / 256, H, F), dim3(256), 0, st, disp, W, H,
+                       dstride, dfstride, q, hm, minbits, xyz, xstride, xfstride);
+}
+
+__global__ void k_disp16_to_f32(const int16_t* d, float* o, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        o[i] = (float)d[i] * 0.0625f;
+}
+
+void launch_disp16_to_f32(const int16_t* d, float* o, size_t n, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_disp16_to_f32, dim3((unsigned)min((n + 255) / 256, (size_t)4096)),
+                       dim3(256), 0, st, d, o, n);
+}
+
+// ------------------------------------------------------------------------------------------
+// A.13 class-path pre-steps
+// ------------------------------------------------------------------------------------------
+__global__ void k_bgr2gray(const uint8_t* bgr, int W, int H, size_t bstride, uint8_t* gray,
+                           size_t gstride) {
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= W) return;
+    const uint8_t* s = bgr + (size_t)f * bstride * H + (size_t)y * bstride + 3 * (size_t)x;
+    int v = (s[0] * 1868 + s[1] * 9617 + s[2] * 4899 + (1 << 13)) >> 14;
+    gray[(size_t)f * gstride * H + (size_t)y * gstride + x] = (uint8_t)v;
+}
+
+__global__ void k_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* dst,
+                            size_t dstride) {
+    const int dw = W / 2, dh = H / 2;
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= dw || y >= dh) return;
+    const uint8_t* a = src + (size_t)f * stride * H + (size_t)(2 * y) * stride + 2 * x;
+    const uint8_t* b = a + stride;
+    dst[(size_t)f * dstride * dh + (size_t)y * dstride + x] = (uint8_t)((a[0] + a[1] + b[0] + b[1] + 2) >> 2);
+}
+
+void launch_bgr2gray(const uint8_t* bgr, int W, int H, size_t bstride, uint8_t* gray,
+                     size_t gstride, int F, hipStream_t st) {
+    hipLaunchKernelGGL(k_bgr2gray, dim3((W + 255) / 256, H, F), dim3(256), 0, st, bgr, W, H,
+                       bstride, gray, gstride);
+}
+
+void launch_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* dst,
+                      size_t dstride, int F, hipStream_t st) {
+    hipLaunchKernelGGL(k_area_half, dim3((W / 2 + 255) / 256, H / 2, F), dim3(256), 0, st, src, W,
+                       H, stride, dst, dstride);
+}
+
+// ------------------------------------------------------------------------------------------
+// self-test of the cross-lane primitives (DPP wave shifts, permlane swaps) on the device
+// ------------------------------------------------------------------------------------------
+__global__ void k_selftest(int* fails, uint32_t seed) {
+    const int lane = threadIdx.x & 63;
+    uint32_t v = (lane * 2654435761u + seed) ^ (seed >> 3);
+    v &= 0x7fff7fffu;
+    uint32_t prev = lane_from_prev(v, kMaxPair);
+    uint32_t next = lane_from_next(v, kMaxPair);
+    // shuffles run on all lanes first (a shuffle inside a divergent branch reads inactive lanes)
+    const uint32_t sp = (uint32_t)__shfl((int)v, (lane + 63) & 63);
+    const uint32_t sn = (uint32_t)__shfl((int)v, (lane + 1) & 63);
+    uint32_t exp_prev = lane == 0 ? kMaxPair : sp;
+    uint32_t exp_next = lane == 63 ? kMaxPair : sn;
+    if (prev != exp_prev) atomicAdd(&fails[0], 1);
+    if (next != exp_next) atomicAdd(&fails[1], 1);
+    uint32_t m = wave_min_pk(v);
+    uint32_t lo = v & 0xffff, hi = v >> 16;
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = min(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    if (m != (lo | (hi << 16))) atomicAdd(&fails[2], 1);
+    uint32_t mu = wave_min_u32(v);
+    uint32_t e = v;
+    for (int o = 32; o > 0; o >>= 1) e = min(e, (uint32_t)__shfl_xor((int)e, o));
+    if (mu != e) atomicAdd(&fails[3], 1);
+}
+
+int selftest_wave_ops(int* failures) {
+    int* d = nullptr;
+    if (hipMalloc(&d, 4 * sizeof(int)) != hipSuccess) return -1;
+    (void)hipMemset(d, 0, 4 * sizeof(int));
+    for (uint32_t s = 1; s < 64; s++) hipLaunchKernelGGL(k_selftest, dim3(4), dim3(256), 0, 0, d, s * 7919u);
+    hipError_t e = hipMemcpy(failures, d, 4 * sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? 0 : -1;
+}
+
+}  // namespace sdr

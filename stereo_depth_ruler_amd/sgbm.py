@@ -31,8 +31,8 @@ except Exception:  # pragma: no cover
 MODE_SGBM, MODE_HH, MODE_SGBM_3WAY, MODE_HH4 = 0, 1, 2, 3
 UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
 # SDR_KERNEL_* (include/sdr/sdr.h)
-(KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATH_WRITE, KERNEL_PATH_ADD, KERNEL_PATH_WTA, KERNEL_LR,
- KERNEL_MEDIAN, KERNEL_SPECKLE, KERNEL_REPROJECT) = range(9)
+(KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATHS, KERNEL_WTA_LR, KERNEL_MEDIAN, KERNEL_SPECKLE,
+ KERNEL_REPROJECT) = range(7)
 
 
 def _is_cuda(x) -> bool:
@@ -188,7 +188,7 @@ class StereoSGBM:
         return disp, xyz
 
     def debug_stage(self, stage: int, shape, dtype):
-        """Copy an internal buffer of the last compute (0 C, 1 raw WTA, 2 LR, 3 final, 4 wta)."""
+        """Copy an internal buffer of the last compute (0 C, 1 raw WTA, 2 LR, 3 final, 4 path costs)."""
         out = np.empty(shape, dtype)
         check(lib().sdr_sgbm_debug_stage(self._h, int(stage), out.ctypes.data, out.nbytes))
         return out

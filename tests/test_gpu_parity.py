@@ -273,7 +273,7 @@ def test_kernel_timing_api():
     m.enable_timing(2)
     m.compute(L, R)
     t, n = m.kernel_time(-1, reset=True)
-    assert n >= 8 and t > 0
+    assert n >= 6 and t > 0  # prefilter, cost, paths, wta+lr, median, speckle
     st = m.last_timing()
     assert st["paths_ms"] > 0
 

@@ -119,7 +119,10 @@ def main():
     import stereo_depth_ruler_amd as sdr
     from stereo_depth_ruler_amd import synthetic as S
     from stereo_depth_ruler_amd.distributed import as_bytes
-    from stereo_depth_ruler_amd.sgbm import KERNEL_PATHS
+    from stereo_depth_ruler_amd import sgbm as _sg
+    KERNEL_KINDS = {"prefilter": _sg.KERNEL_PREFILTER, "k_cost": _sg.KERNEL_COST, "k_paths": _sg.KERNEL_PATHS,
+                    "k_wta_lr": _sg.KERNEL_WTA_LR, "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
+                    "reproject": _sg.KERNEL_REPROJECT}
 
     desc, W, H, args, batch, hm = CONFIGS[a.config]
     D, mode = args[1], args[10]
@@ -177,28 +180,46 @@ def main():
         el = float(t.item())
 
     roofline = None
+    kernels = None
     if not a.no_kernel_timing:
-        tot_ms, cnt = m.kernel_time(KERNEL_PATHS, reset=False)
+        per_kind = {name: m.kernel_time(kind, reset=False) for name, kind in KERNEL_KINDS.items()}
         all_ms, all_cnt = m.kernel_time(-1, reset=True)
         m.enable_timing(0)
+        tot_ms, cnt = per_kind["k_paths"]
         w1 = W - max(args[0] + D, 0) + min(args[0], 0)
         cells = batch * H * w1 * D
-        bytes_per_launch = cells * 6  # C read (2 B) + S read (2 B) + S write (2 B) per cell
+        P = NPATHS[mode]
+        # k_paths: every direction reads C (2 B/cell) and writes its own L_r (2 B/cell)
+        bytes_per_launch = cells * 4 * P
+        kernels = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
+                          "share": round(ms / all_ms, 4) if all_ms else None}
+                   for name, (ms, c) in per_kind.items() if c}
         if cnt:
             avg_s = tot_ms / cnt / 1e3
             achieved = bytes_per_launch / avg_s / 1e9
             roofline = {
                 "bound": "hbm",
-                "kernel": "k_path<DPL=2,S_ADD> (middle path directions, 3 launches/frame)",
+                "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> (all {P} path directions of a batch in one launch)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic("k_path_add"),
+                "traffic": load_traffic(f"{a.config}:k_paths"),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                "bytes_model": f"4*P*cells, P={P}, cells=batch*H*W1*D={cells}",
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "launches_timed": cnt,
                 "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
+            }
+            # whole pipeline against the canonical 2+6P B/cell model (cost write, path C read +
+            # L write, WTA L read), over the summed kernel time of a step
+            pipe_bytes = cells * (2 + 6 * P)
+            gpu_s = all_ms / 1e3 / max(1, a.steps)
+            roofline["pipeline"] = {
+                "algorithmic_bytes_per_step": pipe_bytes,
+                "kernel_time_per_step_us": round(gpu_s * 1e6, 1),
+                "achieved": round(pipe_bytes / gpu_s / 1e9, 1),
+                "frac": round(pipe_bytes / gpu_s / 1e9 / HBM_PEAK_GBS, 4),
             }
 
     pix = world * a.steps * batch * W * H
@@ -227,6 +248,7 @@ def main():
         },
         "fps": round(world * a.steps * batch / el, 2),
         "roofline": roofline,
+        "kernels": kernels,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -118,6 +118,12 @@ int sdr_reproject_device(const float* d_disp, int width, int height, size_t disp
 int sdr_disp16_reproject_device(const int16_t* d_disp, int width, int height, size_t disp_stride,
                                 const double Q[16], int handle_missing, float* d_xyz,
                                 size_t xyz_stride, int nframes, void* stream);
+/* cv::filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on dense int16 frames [nframes][H][W],
+ * in place, asynchronous on `stream`.  This is the post-filter StereoSGBM::compute applies with
+ * newVal = (minDisparity-1)*16, maxDiff = 16*speckleRange; scratch is
+ * stream-ordered (hipMallocAsync). */
+int sdr_filter_speckles_device(int16_t* d_img, int width, int height, int nframes, int newVal,
+                               int maxSpeckleSize, int maxDiff, void* stream);
 /* disp.convertTo(f, CV_32F, 1/16) on device. */
 int sdr_disp16_to_float_device(const int16_t* d_disp, float* d_out, size_t n, void* stream);
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# PMC passes (one counter group per rocprofv3 run; --pmc never combined with tracing domains).
+# usage: scripts/pmc_profile.sh <outdir> [bench args...]
+set -e
+OUT=${1:-gpurun_out/pmc}; shift || true
+ARGS=${@:---steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p "$OUT"
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+done
+echo pmc-done

@@ -5,11 +5,11 @@ HIP/CDNA4 kernels behind a C ABI (include/sdr/sdr.h), with an OpenCV-shaped Pyth
 from ._lib import SDRError, SgbmParams, LIB_PATH  # noqa: F401
 from .sgbm import (  # noqa: F401
     MODE_HH, MODE_HH4, MODE_SGBM, MODE_SGBM_3WAY, StereoSGBM, createRightMatcher,
-    cvt_bgr2gray, disparity_to_float, reprojectImageTo3D, resize_area_half,
+    cvt_bgr2gray, disparity_to_float, filterSpeckles, reprojectImageTo3D, resize_area_half,
 )
 
 __all__ = [
     "SDRError", "SgbmParams", "StereoSGBM", "createRightMatcher", "reprojectImageTo3D",
-    "disparity_to_float", "cvt_bgr2gray", "resize_area_half",
+    "disparity_to_float", "filterSpeckles", "cvt_bgr2gray", "resize_area_half",
     "MODE_SGBM", "MODE_HH", "MODE_SGBM_3WAY", "MODE_HH4",
 ]

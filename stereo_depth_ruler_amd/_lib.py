@@ -62,6 +62,7 @@ SIGNATURES = [
     ("sdr_disp16_reproject_device", _i,
      [_vp, _i, _i, _sz, _c.POINTER(_c.c_double), _i, _vp, _sz, _i, _vp]),
     ("sdr_disp16_to_float_device", _i, [_vp, _vp, _sz, _vp]),
+    ("sdr_filter_speckles_device", _i, [_vp, _i, _i, _i, _i, _i, _i, _vp]),
     ("sdr_bgr2gray_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
     ("sdr_resize_area_half_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
     ("sdr_stereo_class_compute", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _sz, _vp, _vp]),

@@ -9,7 +9,10 @@
 // Cost kernel: lanes = disparity pairs (as in the path kernels), each wave walks CW output
 // columns; the horizontal window and the vertical running sum live in registers (static ring
 // slots by unrolling the row loop by the window height), the right image's pair planes for the
-// block's column span are staged in LDS (double-buffered, one barrier per row).
+// block's column span are staged in LDS (double-buffered, one barrier per row). The staged R
+// pair planes are split into even/odd-x halves: lane p reads entry x - 2p, so with the split
+// adjacent lanes read adjacent 8-byte words and ds_read_b64 is bank-conflict free (interleaved,
+// the -16 B lane stride hits each bank pair twice per 32-lane group).
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 
@@ -106,6 +109,10 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
 // The window is walked over "virtual" rows q = t-SH2 .. t+SH2 (physical row clamp(q, s0, H-1)),
 // so the ring of the last NR rows is a plain sliding window with compile-time slots.
 // ------------------------------------------------------------------------------------------
+// parity half of a staged R plane: >= ceil(STR/2), == 16 (mod 32) so the even/odd halves of a
+// 32-lane staging store land on disjoint banks
+__host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 15) / 32 * 32 + 16; }
+
 template <int K>
 struct CostCfg {
     static constexpr int CW = K == 1 ? 8 : 4;  // output columns per wave
@@ -163,6 +170,8 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     const int xr_lo = mlo + g.minX1 - g.minD - (D - 2);
     const int NRP = NL + D - 2;
     const int STR = BCOLS + 2 * SW2 + D;
+    const int HR = cost_half_r(STR);  // entries per parity half of a staged R plane
+    const int BUF = 3 * STR + 6 * HR;
     const uint64_t* PLf = a.pl.L + (size_t)f * a.pl.fstrideL;
     const uint64_t* PRf = a.pl.R + (size_t)f * a.pl.fstrideR;
     const size_t plane = (size_t)H * W;
@@ -185,7 +194,8 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
             }
     };
     auto put = [&](int b) {
-        uint64_t* B = lds + (size_t)b * 6 * STR;
+        uint64_t* B = lds + (size_t)b * BUF;
+        uint64_t* BR = B + 3 * STR;
         if (tid < NL) {
 #pragma unroll
             for (int k = 0; k < 3; k++) B[k * STR + tid] = ql[k];
@@ -195,7 +205,7 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
 #pragma unroll
             for (int t = 0; t < NPR; t++) {
                 const int i = tid + 256 * t;
-                if (i < NRP) B[(3 + k) * STR + i] = qr[k][t];
+                if (i < NRP) BR[k * 2 * HR + (i & 1) * HR + (i >> 1)] = qr[k][t];
             }
     };
 
@@ -206,8 +216,17 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     for (int i = 0; i < K; i++) {
         const int qp = lane + 64 * i;
         act[i] = 2 * qp < D;
-        // staged R index of xr = minX1 + m - minD - 2qp is (m - mlo) + (D - 2 - 2qp)
-        xoff[i] = act[i] ? D - 2 - 2 * qp : 0;
+        // staged R index of xr = minX1 + m - minD - 2qp is (m - mlo) + (D - 2 - 2qp): same parity
+        // as m - mlo, position (parity half) + ((m - mlo) >> 1) + (D - 2) / 2 - qp
+        xoff[i] = act[i] ? (D - 2) / 2 - qp : 0;
+    }
+    // per-column staged offsets (uniform, loop invariant)
+    int colL[NC], colR[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+        const int li = min(max(wx0 - SW2 + j, 0), W1 - 1) - mlo;
+        colL[j] = __builtin_amdgcn_readfirstlane(li);
+        colR[j] = __builtin_amdgcn_readfirstlane(3 * STR + (li & 1) * HR + (li >> 1));
     }
 
     // virtual rows and outputs
@@ -240,25 +259,22 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
             put(b ^ 1);
             if (q + 2 <= qend) fetch(phys(q + 2));
         }
-        const uint64_t* B = lds + (size_t)b * 6 * STR;
+        const uint64_t* B = lds + (size_t)b * BUF;
         // pixel costs of the NC columns of this wave, then the horizontal window sums
         uint32_t hs[K][CW];
         uint32_t pix[K][NC];
 #pragma unroll
         for (int j = 0; j < NC; j++) {
-            const int m = min(max(wx0 - SW2 + j, 0), W1 - 1);
-            const int li = __builtin_amdgcn_readfirstlane(m - mlo);
+            const int li = colL[j];
+            // broadcast LDS reads (every lane the same address): the L operands stay in VGPRs so
+            // several columns' loads can be in flight (no readfirstlane wait per column)
             const uint64_t l0 = B[li], l1 = B[STR + li], l2 = B[2 * STR + li];
-            const uint32_t u = __builtin_amdgcn_readfirstlane((uint32_t)l0);
-            const uint32_t u0 = __builtin_amdgcn_readfirstlane((uint32_t)(l0 >> 32));
-            const uint32_t u1 = __builtin_amdgcn_readfirstlane((uint32_t)l1);
-            const uint32_t ur = __builtin_amdgcn_readfirstlane((uint32_t)(l1 >> 32));
-            const uint32_t ur0 = __builtin_amdgcn_readfirstlane((uint32_t)l2);
-            const uint32_t ur1 = __builtin_amdgcn_readfirstlane((uint32_t)(l2 >> 32));
+            const uint32_t u = (uint32_t)l0, u0 = (uint32_t)(l0 >> 32), u1 = (uint32_t)l1;
+            const uint32_t ur = (uint32_t)(l1 >> 32), ur0 = (uint32_t)l2, ur1 = (uint32_t)(l2 >> 32);
 #pragma unroll
             for (int i = 0; i < K; i++) {
-                const int xi = li + xoff[i];
-                const uint64_t r0 = B[3 * STR + xi], r1 = B[4 * STR + xi], r2 = B[5 * STR + xi];
+                const int xi = colR[j] + xoff[i];
+                const uint64_t r0 = B[xi], r1 = B[2 * HR + xi], r2 = B[4 * HR + xi];
                 const uint32_t bs = bt_cost(u, u0, u1, (uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1);
                 const uint32_t br = bt_cost(ur, ur0, ur1, (uint32_t)(r1 >> 32), (uint32_t)r2, (uint32_t)(r2 >> 32));
                 pix[i][j] = pk_add(bs, as_u32(as_s16x2(br) >> (short)2));
@@ -306,12 +322,30 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
 }
 
 template <int NR, int K>
-static void launch_cost_t(const Geometry& g, const CostArgs& a, int F, hipStream_t st) {
+static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) {
     constexpr int BCOLS = 4 * CostCfg<K>::CW;
     const int rows = a.row_end - a.row_begin;
-    dim3 grid((g.W1 + BCOLS - 1) / BCOLS, (rows + a.TY - 1) / a.TY, F);
     const int STR = BCOLS + 2 * ((NR - 1) / 2) + g.D;
-    hipLaunchKernelGGL((k_cost<NR, K>), grid, dim3(256), (size_t)2 * 6 * STR * 8, st, g, a);
+    const size_t lds = (size_t)2 * (3 * STR + 6 * cost_half_r(STR)) * 8;
+    const int colblocks = (g.W1 + BCOLS - 1) / BCOLS;
+    if (a.TY <= 0) {
+        // one full pass of resident blocks: a partial second pass doubles the kernel time, and
+        // each block re-walks NR-1 warm-up rows, so use the tallest row band that fills the chip
+        static thread_local size_t key = 0;
+        static thread_local int slots = 0;
+        if (key != lds) {
+            int dev = 0, cus = 0, per_cu = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_cost<NR, K>, 256, lds);
+            slots = max(1, cus * max(1, per_cu));
+            key = lds;
+        }
+        const int bands = max(1, slots / max(1, colblocks * F));
+        a.TY = max(4, (rows + bands - 1) / bands);
+    }
+    dim3 grid(colblocks, (rows + a.TY - 1) / a.TY, F);
+    hipLaunchKernelGGL((k_cost<NR, K>), grid, dim3(256), lds, st, g, a);
 }
 
 bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.SH2 <= 5 && g.D <= 256; }

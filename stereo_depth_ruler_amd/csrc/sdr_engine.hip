@@ -193,8 +193,11 @@ static int npaths_of(int mode) { return mode == SDR_MODE_HH ? 8 : mode == SDR_MO
 //   each into its own L buffer -> WTA/uniqueness/subpixel/disp2/LR per row -> median3 -> speckle
 // Per cell this moves 2 (C write) + 4P (paths: C read + L write) + 2P (WTA: L reads) bytes,
 // the canonical 2 + 6P of SURVEY.md 8(d).
+//   out (nullable): dense [F][H][W] int16 destination for the final map (else internal buffer)
+//   out_min (nullable): per-frame minimum of the final map (reprojectImageTo3D handleMissing)
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
-                           size_t stride, size_t fstride, int F, int16_t** final_disp) {
+                           size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
+                           int16_t** final_disp) {
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
@@ -203,9 +206,11 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     const size_t px = (size_t)W * H;
     if ((rc = ensure(h->dfin, F * px * 2))) return rc;
     int16_t* dfin = (int16_t*)h->dfin.p;
-    *final_disp = dfin;
+    int16_t* dst = out ? out : dfin;
+    *final_disp = dst;
     if (g.W1 <= 0) {
-        sdr::launch_fill_s16(dfin, (int16_t)e.invalid, F * px, st);
+        sdr::launch_fill_s16(dst, (int16_t)e.invalid, F * px, st);
+        if (out_min) sdr::launch_min_s16(dst, px, px, F, out_min, st);
         return SDR_OK;
     }
     if (g.W1 <= g.SW2) return fail(SDR_ERR_SIZE, "image too narrow for numDisparities/blockSize");
@@ -256,7 +261,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     ca.s0 = 0;
     ca.ylim = std::max(H - 1 - g.SH2, 0);
     ca.hh_bottom = e.mode == SDR_MODE_HH;
-    ca.TY = 32;
+    ca.TY = 0;  // sized by launch_cost for one full pass of resident blocks
     { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
     for (size_t s = 0; s < stripes.size(); s++) {
         const Stripe& sp = stripes[s];
@@ -338,11 +343,15 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     wa.uniq_simd = e.uniq_simd;
     wa.disp12MaxDiff = e.disp12MaxDiff;
     { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_wta_lr(g, wa, F, st); }
-    { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, dfin, W, H, F, st); }
-    if (e.speckle_ws > 0) {
+    const bool speckle = e.speckle_ws > 0;
+    { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, speckle ? dfin : dst, W, H, F, st); }
+    if (speckle) {
         KTimer kt(h, SDR_KERNEL_SPECKLE);
-        sdr::launch_speckle(dfin, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
-                            (int*)h->labels.p, (int*)h->sizes.p, st);
+        sdr::launch_speckle(dfin, dst, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
+                            (int*)h->labels.p, (int*)h->sizes.p, out_min, st);
+    } else if (out_min) {
+        KTimer kt(h, SDR_KERNEL_REPROJECT);
+        sdr::launch_min_s16(dst, px, px, F, out_min, st);
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
     SDR_HIP(hipGetLastError());
@@ -491,11 +500,11 @@ int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, i
     if (F > 1 && fstride < stride * H) return fail(SDR_ERR_ARG, "frame_stride too small");
     SDR_HIP(hipSetDevice(h->device));
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, &fin))) return rc;
     const size_t px = (size_t)W * H;
-    if (disp_stride == (size_t)W && (F == 1 || disp_fstride == px)) {
-        SDR_HIP(hipMemcpyAsync(dDisp, fin, F * px * 2, hipMemcpyDeviceToDevice, h->stream));
-    } else {
+    const bool dense = disp_stride == (size_t)W && (F == 1 || disp_fstride == px);
+    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, dense ? dDisp : nullptr, nullptr, &fin)))
+        return rc;
+    if (!dense) {
         for (int f = 0; f < F; f++)
             SDR_HIP(hipMemcpy2DAsync(dDisp + f * disp_fstride, disp_stride * 2, fin + f * px, W * 2,
                                      W * 2, H, hipMemcpyDeviceToDevice, h->stream));
@@ -512,16 +521,15 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint
     if (F > 1 && fstride < stride * H) return fail(SDR_ERR_ARG, "frame_stride too small");
     SDR_HIP(hipSetDevice(h->device));
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, &fin))) return rc;
     const size_t px = (size_t)W * H;
     if ((rc = ensure(h->mins, (size_t)F * 4))) return rc;
+    int* mins = handle_missing ? (int*)h->mins.p : nullptr;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, dDisp, mins, &fin))) return rc;
     {
         KTimer kt(h, SDR_KERNEL_REPROJECT);
-        if (handle_missing) sdr::launch_min_s16(fin, px, px, F, (int*)h->mins.p, h->stream);
-        sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, (const int*)h->mins.p, dXYZ,
-                                  (size_t)W * 3, px * 3, F, h->stream);
+        sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, mins, dXYZ, (size_t)W * 3,
+                                  px * 3, F, h->stream);
     }
-    if (dDisp) SDR_HIP(hipMemcpyAsync(dDisp, fin, F * px * 2, hipMemcpyDeviceToDevice, h->stream));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -541,7 +549,7 @@ int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int
     SDR_HIP(hipMemcpy2DAsync(dL, W, left, stride, W, H, hipMemcpyHostToDevice, h->stream));
     SDR_HIP(hipMemcpy2DAsync(dR, W, right, stride, W, H, hipMemcpyHostToDevice, h->stream));
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, &fin))) return rc;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, nullptr, &fin))) return rc;
     SDR_HIP(hipMemcpy2DAsync(disp, disp_stride * 2, fin, W * 2, W * 2, H, hipMemcpyDeviceToHost,
                              h->stream));
     SDR_HIP(hipStreamSynchronize(h->stream));
@@ -560,6 +568,24 @@ int sdr_reproject_device(const float* d_disp, int W, int H, size_t disp_stride, 
     sdr::launch_reproject_f32(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,
                               d_xyz, xyz_stride, xyz_stride * H, F, (hipStream_t)stream);
     if (mins) SDR_HIP(hipFreeAsync(mins, (hipStream_t)stream));
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_filter_speckles_device(int16_t* d_img, int W, int H, int F, int newVal, int maxSpeckleSize,
+                               int maxDiff, void* stream) {
+    if (!d_img) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, (size_t)W, F);
+    if (rc) return rc;
+    if ((size_t)W * H > (size_t)INT32_MAX) return fail(SDR_ERR_SIZE, "frame too large");
+    if (maxSpeckleSize <= 0) return SDR_OK;  // OpenCV: nothing to do
+    hipStream_t st = (hipStream_t)stream;
+    const size_t n = (size_t)F * W * H;
+    int* scratch = nullptr;
+    SDR_HIP(hipMallocAsync((void**)&scratch, n * 8, st));
+    sdr::launch_speckle(d_img, d_img, W, H, F, newVal, maxSpeckleSize, maxDiff, scratch, scratch + n,
+                        nullptr, st);
+    SDR_HIP(hipFreeAsync(scratch, st));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -675,13 +701,13 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
     // matcher->compute(L, R) (stereo_disparity.cpp:27)
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, &fin))) return rc;
+    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, nullptr, nullptr, &fin))) return rc;
     SDR_HIP(hipMemcpyAsync(dl, fin, px2 * 2, hipMemcpyDeviceToDevice, st));
     if (right) {
         // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
         hipStream_t rs = right->stream;
         right->stream = st;
-        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, &fin);
+        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, nullptr, nullptr, &fin);
         right->stream = rs;
         if (rc) return rc;
         SDR_HIP(hipMemcpyAsync(dr, fin, px2 * 2, hipMemcpyDeviceToDevice, st));

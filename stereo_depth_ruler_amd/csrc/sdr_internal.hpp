@@ -85,8 +85,9 @@ void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
-void launch_speckle(int16_t* img, int W, int H, int F, int newVal, int maxSize, int maxDiff,
-                    int* labels, int* sizes, hipStream_t st);
+// src may equal dst; out_min (nullable) receives min over each output frame
+void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
+                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st);
 void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
                     hipStream_t st);
 void launch_reproject_s16(const int16_t* disp, int W, int H, size_t dstride, size_t dfstride,

@@ -41,18 +41,33 @@ void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipSt
 // ------------------------------------------------------------------------------------------
 // A.11 filterSpeckles as connected-component labelling: 4-neighbours p,q are joined iff
 // neither equals newVal and |v(p)-v(q)| <= maxDiff; components of <= maxSize pixels are set to
-// newVal.  Lock-free union-find with atomicMin (Playne & Hawick 2018), then flatten, count,
-// apply.  The flood fill of OpenCV and CCL give identical components (the join relation is
+// newVal.  The flood fill of OpenCV and CCL give identical components (the join relation is
 // symmetric and evaluated on the unmodified image).
+//
+//   k_ccl_local    32x32 tile in LDS: horizontal runs from one ballot per row (no atomics), run
+//                  unions across rows (lock-free union-find, Playne & Hawick 2018), local sizes
+//                  with one LDS atomic per (wave, root).  P[pixel] = tile-root pixel index,
+//                  S[tile root] = its pixel count, S = 0 elsewhere.
+//   k_ccl_merge    tile-border pixel pairs unite the tile roots (global union-find); a pair whose
+//                  previous pair along the border is joined through in-tile edges is skipped.
+//   k_ccl_finalize each tile root finds its global root, adds its count there, points at it.
+//   k_ccl_apply    P[P[pixel]] is the global root -> size test -> output (+ fused frame minimum
+//                  for reprojectImageTo3D's handleMissingValues).
+// Pixel-level work is streaming; global finds and atomics scale with the number of tile
+// components, not with the pixels of a large component.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int uf_load(int* P, int i) {
+__device__ __forceinline__ int uf_load(const int* P, int i) {
     return __hip_atomic_load(&P[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// find with path halving; parents only ever decrease (union links the larger root under the
+// smaller), so a no-return atomicMin keeps concurrent unions intact
 __device__ __forceinline__ int uf_find(int* P, int x) {
     int p = uf_load(P, x);
     while (p != x) {
+        const int gp = uf_load(P, p);
+        if (gp != p) atomicMin(&P[x], gp);
         x = p;
-        p = uf_load(P, x);
+        p = gp;
     }
     return x;
 }
@@ -73,8 +88,6 @@ __device__ __forceinline__ void uf_unite(int* P, int a, int b) {
     }
 }
 
-// Tile-local pass: 32x32 tile in LDS, union-find with LDS atomics, roots written as global
-// pixel indices.  Then only tile borders are merged with global atomics.
 constexpr int kCT = 32;
 
 __device__ __forceinline__ int lds_find(int* lab, int x) {
@@ -102,112 +115,171 @@ __device__ __forceinline__ void lds_unite(int* lab, int a, int b) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_ccl_local(const int16_t* img, int* P, int* sizes, int W,
-                                                   int H, int newVal, int maxDiff) {
-    __shared__ int16_t v[kCT * kCT];
+__device__ __forceinline__ bool joined(int a, int b, int newVal, int maxDiff) {
+    return a != newVal && b != newVal && abs(a - b) <= maxDiff;
+}
+
+// 256 threads = 4 waves; pixel i = t + 256k (k < 4): a wave covers two tile rows per k
+__global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ img, int* __restrict__ P,
+                                                   int* __restrict__ S, int W, int H, int newVal,
+                                                   int maxDiff, int* out_min) {
+    __shared__ int v[kCT * kCT];
     __shared__ int lab[kCT * kCT];
+    __shared__ int cnt[kCT * kCT];
     const int tx0 = blockIdx.x * kCT, ty0 = blockIdx.y * kCT;
     const size_t fo = (size_t)blockIdx.z * W * H;
-    const int16_t* I = img + fo;
-    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
-        const int gx = tx0 + (i & (kCT - 1)), gy = ty0 + (i >> 5);
-        int val = newVal;
-        if (gx < W && gy < H) val = I[(size_t)gy * W + gx];
-        v[i] = (int16_t)val;
-        lab[i] = val != newVal ? i : -1;
+    const int t = threadIdx.x, lane = t & 63, lx = t & (kCT - 1);
+    if (out_min && t == 0 && blockIdx.x == 0 && blockIdx.y == 0) out_min[blockIdx.z] = 32767;
+    const int gx = tx0 + lx;
+    int val[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = t + 256 * k, gy = ty0 + (i >> 5);
+        val[k] = (gx < W && gy < H) ? (int)img[fo + (size_t)gy * W + gx] : newVal;
+        v[i] = val[k];
+        cnt[i] = 0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
-        if (lab[i] < 0) continue;
-        const int lx = i & (kCT - 1), ly = i >> 5;
-        const int val = v[i];
-        if (lx + 1 < kCT && lab[i + 1] >= 0 && abs(val - v[i + 1]) <= maxDiff) lds_unite(lab, i, i + 1);
-        if (ly + 1 < kCT && lab[i + kCT] >= 0 && abs(val - v[i + kCT]) <= maxDiff) lds_unite(lab, i, i + kCT);
+    // horizontal runs: a run starts at every valid pixel not joined to its left neighbour
+    int run[4];
+    bool hc[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = t + 256 * k;
+        const bool valid = val[k] != newVal;
+        hc[k] = valid && lx > 0 && joined(val[k], v[i - 1], newVal, maxDiff);
+        const unsigned long long starts = __ballot(valid && !hc[k]);
+        const unsigned long long below = starts & (~0ull >> (63 - lane));
+        const int s = 63 - __clzll(below);  // the row's first valid pixel is a start: below != 0
+        run[k] = valid ? i - (lane - s) : -1;
+        lab[i] = run[k];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kCT * kCT; i += 256) {
-        const int gx = tx0 + (i & (kCT - 1)), gy = ty0 + (i >> 5);
-        if (gx >= W || gy >= H) continue;
-        const size_t g = (size_t)gy * W + gx;
-        int r = -1;
-        if (lab[i] >= 0) {
-            const int lr = lds_find(lab, i);
-            r = (ty0 + (lr >> 5)) * W + tx0 + (lr & (kCT - 1));
+    // vertical joins between runs; skip the join when the left pixel (same run) is joined to the
+    // up-left pixel (same run as up): those two runs are already being united
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = t + 256 * k;
+        if (run[k] < 0 || i < kCT) continue;
+        const int up = i - kCT, vu = v[up];
+        if (!joined(val[k], vu, newVal, maxDiff)) continue;
+        if (hc[k]) {
+            const int vl = v[i - 1], vul = v[up - 1];
+            if (joined(vl, vul, newVal, maxDiff) && joined(vu, vul, newVal, maxDiff)) continue;
         }
-        P[fo + g] = r;
-        sizes[fo + g] = 0;
+        lds_unite(lab, run[k], up);
+    }
+    __syncthreads();
+    // roots and local sizes (one LDS atomic per distinct root of a wave)
+    int root[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        root[k] = run[k] >= 0 ? lds_find(lab, run[k]) : -1;
+        unsigned long long pend = __ballot(root[k] >= 0);
+        while (pend) {
+            const int src = __ffsll((long long)pend) - 1;
+            const int r = __shfl(root[k], src);
+            const unsigned long long m = __ballot(root[k] == r) & pend;
+            if (lane == src) atomicAdd(&cnt[r], __popcll(m));
+            pend &= ~m;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = t + 256 * k, gy = ty0 + (i >> 5);
+        if (gx >= W || gy >= H) continue;
+        const size_t g = fo + (size_t)gy * W + gx;
+        const int r = root[k];
+        P[g] = r >= 0 ? (ty0 + (r >> 5)) * W + tx0 + (r & (kCT - 1)) : -1;
+        S[g] = (r >= 0 && r == i) ? cnt[i] : 0;
     }
 }
 
-// merge across tile borders: vertical borders (x = 32k-1 | 32k) and horizontal ones
-__global__ void k_ccl_merge(const int16_t* img, int* P, int W, int H, int newVal, int maxDiff) {
+// tile-border pairs: vertical borders (x = 32k-1 | 32k) and horizontal ones (y = 32k-1 | 32k)
+__global__ __launch_bounds__(256) void k_ccl_merge(const int16_t* __restrict__ img, int* P, int W,
+                                                   int H, int newVal, int maxDiff) {
     const size_t fo = (size_t)blockIdx.y * W * H;
     const int16_t* I = img + fo;
     int* Pf = P + fo;
     const int nvx = (W - 1) / kCT, nhy = (H - 1) / kCT;
     const int nv = nvx * H, nh = nhy * W;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nv + nh; t += gridDim.x * blockDim.x) {
-        int a, b;
+        int a, b, step;
+        bool inner;  // the previous pair along the border is tied to this one by in-tile edges
         if (t < nv) {
-            const int y = t / nvx, x = (t - y * nvx + 1) * kCT - 1;
+            const int xb = t % nvx, y = t / nvx, x = (xb + 1) * kCT - 1;
             a = y * W + x;
             b = a + 1;
+            step = W;
+            inner = (y % kCT) != 0;
         } else {
             const int u = t - nv;
-            const int yb = u / W, x = u - yb * W;
-            const int y = (yb + 1) * kCT - 1;
+            const int yb = u / W, x = u - yb * W, y = (yb + 1) * kCT - 1;
             a = y * W + x;
             b = a + W;
+            step = 1;
+            inner = (x % kCT) != 0;
         }
         const int va = I[a], vb = I[b];
-        if (va != newVal && vb != newVal && abs(va - vb) <= maxDiff) uf_unite(Pf, a, b);
+        if (!joined(va, vb, newVal, maxDiff)) continue;
+        if (inner) {
+            const int pa = I[a - step], pb = I[b - step];
+            if (joined(pa, pb, newVal, maxDiff) && joined(va, pa, newVal, maxDiff) &&
+                joined(vb, pb, newVal, maxDiff))
+                continue;
+        }
+        uf_unite(Pf, a, b);
     }
 }
 
-// flatten to roots and count component sizes with one atomic per (wave, root)
-__global__ void k_ccl_count(int* P, int* sizes, int n) {
+// tile roots (S > 0): global root, size accumulated there, one-hop pointer for apply
+__global__ __launch_bounds__(256) void k_ccl_finalize(int* P, int* S, int n) {
     const size_t fo = (size_t)blockIdx.y * n;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int r = -1;
-    if (i < n) {
-        r = P[fo + i];
-        if (r >= 0) {
-            r = uf_find(P + fo, r);
-            P[fo + i] = r;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int c = S[fo + i];
+        if (c <= 0) continue;
+        const int g = uf_find(P + fo, i);
+        if (g != i) {
+            atomicAdd(&S[fo + g], c);
+            P[fo + i] = g;
         }
     }
-    unsigned long long pend = __ballot(r >= 0);
-    const int lane = threadIdx.x & 63;
-    while (pend) {
-        const int src = __ffsll((long long)pend) - 1;
-        const int lr = __shfl(r, src);
-        const unsigned long long m = __ballot(r == lr) & pend;
-        if (lane == src) atomicAdd(&sizes[fo + lr], __popcll(m));
-        pend &= ~m;
-    }
 }
 
-__global__ void k_ccl_apply(int16_t* img, const int* P, const int* sizes, int n, int newVal,
-                            int maxSize) {
+__global__ __launch_bounds__(256) void k_ccl_apply(const int16_t* src, int16_t* dst, const int* P,
+                                                   const int* S, int n, int newVal, int maxSize,
+                                                   int* out_min) {
+    __shared__ int wm[4];
     const size_t fo = (size_t)blockIdx.y * n;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int r = P[fo + i];
-    if (r >= 0 && sizes[fo + r] <= maxSize) img[fo + i] = (int16_t)newVal;
+    int m = 32767;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        int v = src[fo + i];
+        const int l = P[fo + i];
+        if (l >= 0 && S[fo + P[fo + l]] <= maxSize) v = newVal;
+        dst[fo + i] = (int16_t)v;
+        m = min(m, v);
+    }
+    if (!out_min) return;
+    m = (int)wave_min_u32((uint32_t)(m + 32768)) - 32768;
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMin(&out_min[blockIdx.y], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
 }
 
-void launch_speckle(int16_t* img, int W, int H, int F, int newVal, int maxSize, int maxDiff,
-                    int* labels, int* sizes, hipStream_t st) {
+void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
+                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st) {
     const int n = W * H;
     hipLaunchKernelGGL(k_ccl_local, dim3((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, F), dim3(256), 0,
-                       st, img, labels, sizes, W, H, newVal, maxDiff);
+                       st, src, labels, sizes, W, H, newVal, maxDiff, out_min);
     const int nb = ((W - 1) / kCT) * H + ((H - 1) / kCT) * W;
     if (nb > 0)
         hipLaunchKernelGGL(k_ccl_merge, dim3((unsigned)min((nb + 255) / 256, 1024), F), dim3(256), 0,
-                           st, img, labels, W, H, newVal, maxDiff);
-    hipLaunchKernelGGL(k_ccl_count, dim3((n + 255) / 256, F), dim3(256), 0, st, labels, sizes, n);
-    hipLaunchKernelGGL(k_ccl_apply, dim3((n + 255) / 256, F), dim3(256), 0, st, img, labels, sizes, n,
-                       newVal, maxSize);
+                           st, src, labels, W, H, newVal, maxDiff);
+    const unsigned gb = (unsigned)min((n + 1023) / 1024, 256);
+    hipLaunchKernelGGL(k_ccl_finalize, dim3(gb, F), dim3(256), 0, st, labels, sizes, n);
+    hipLaunchKernelGGL(k_ccl_apply, dim3(gb, F), dim3(256), 0, st, src, dst, labels, sizes, n, newVal,
+                       maxSize, out_min);
 }
 
 // ------------------------------------------------------------------------------------------

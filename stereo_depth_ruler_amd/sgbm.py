@@ -266,6 +266,21 @@ def reproject_disp16(disp16, Q, handleMissingValues=False):
     return out[0] if squeeze else out
 
 
+def filterSpeckles(img, newVal, maxSpeckleSize, maxDiff):
+    """cv::filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) in place on a CUDA int16 tensor
+    (H, W) or (F, H, W): 4-connected components of pixels that differ by <= maxDiff, excluding
+    newVal pixels, of <= maxSpeckleSize pixels are set to newVal.  Returns img."""
+    if not _is_cuda(img) or img.dtype != torch.int16 or not img.is_contiguous():
+        raise SDRError(-5, "filterSpeckles expects a contiguous CUDA int16 tensor")
+    if img.dim() not in (2, 3):
+        raise SDRError(-1, "filterSpeckles expects (H, W) or (F, H, W)")
+    f = 1 if img.dim() == 2 else img.shape[0]
+    h, w = img.shape[-2:]
+    check(lib().sdr_filter_speckles_device(img.data_ptr(), w, h, f, int(newVal), int(maxSpeckleSize),
+                                           int(maxDiff), _cstream(img.device.index)))
+    return img
+
+
 def disparity_to_float(disp16):
     """disp.convertTo(f, CV_32F, 1/16) (device tensors stay on device)."""
     if _is_cuda(disp16):

@@ -116,21 +116,50 @@ __host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 15
 template <int K>
 struct CostCfg {
     static constexpr int CW = K == 1 ? 8 : 4;  // output columns per wave
+    // waves per SIMD the register budget is capped for (the ring holds NR x K x CW pairs)
+    static constexpr int waves(int NR) { return NR * K <= 5 ? 3 : (NR * K <= 14 ? 2 : 1); }
 };
 
+// Birchfield-Tomasi dissimilarity of packed pairs: min(max(0, u-v1, v0-u), max(0, v-u1, u0-v)).
+// Operands are in [0, 255], so max(x, 0) of a difference is an unsigned saturating subtract and
+// one of each pair is zero: 4 v_pk_sub_u16 (clamp) + 2 v_pk_max_u16 + 1 v_pk_min_u16.
 __device__ __forceinline__ uint32_t bt_cost(uint32_t u, uint32_t u0, uint32_t u1, uint32_t v,
                                             uint32_t v0, uint32_t v1) {
-    const uint32_t c0 = pk_max(pk_max(pk_sub(u, v1), pk_sub(v0, u)), 0u);
-    const uint32_t c1 = pk_max(pk_max(pk_sub(v, u1), pk_sub(u0, v)), 0u);
-    return pk_min(c0, c1);
+    const uint32_t c0 = pk_max_u(pk_sub_usat(u, v1), pk_sub_usat(v0, u));
+    const uint32_t c1 = pk_max_u(pk_sub_usat(v, u1), pk_sub_usat(u0, v));
+    return pk_min_u(c0, c1);
+}
+
+// pix[j] = pix[src] for the columns a block-edge wave sees beyond the image (x clamped to
+// [0, W1-1]): J0 = first in-image column (left edge), J1 = last in-image column (right edge)
+template <int K, int NC, int J0>
+__device__ __forceinline__ void clamp_left(uint32_t (&pix)[K][NC]) {
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
+        for (int j = 0; j < J0; j++) pix[i][j] = pix[i][J0];
+}
+template <int K, int NC, int J1>
+__device__ __forceinline__ void clamp_right(uint32_t (&pix)[K][NC]) {
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
+        for (int j = J1 + 1; j < NC; j++) pix[i][j] = pix[i][J1];
+}
+template <int K, int NC, int... J>
+__device__ __forceinline__ void clamp_edges(uint32_t (&pix)[K][NC], int j0, int j1,
+                                            std::integer_sequence<int, J...>) {
+    ((j0 == J ? clamp_left<K, NC, J>(pix) : void()), ...);
+    ((j1 == J ? clamp_right<K, NC, J>(pix) : void()), ...);
 }
 
 template <int NR, int K>
-__global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CostCfg<K>::waves(NR)))) void k_cost(Geometry g, CostArgs a) {
     constexpr int SW2 = (NR - 1) / 2, SH2 = SW2;
     constexpr int CW = CostCfg<K>::CW;
     constexpr int NC = CW + 2 * SW2;
     constexpr int BCOLS = 4 * CW;
+    constexpr int NLV = BCOLS + 2 * SW2;  // staged (virtual) columns of a block
     extern __shared__ uint64_t lds[];
     const int W = g.W, H = g.H, W1 = g.W1, D = g.D;
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
@@ -144,31 +173,39 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     const uint32_t P2x2 = splat16(g.P2);
     int16_t* out = a.out + (size_t)f * a.out_fstride;
 
-    // rows [yl, ty1) of MODE_HH keep the initial P2
-    int yl = ty1;
-    if (a.hh_bottom) yl = max(ty0, min(ty1, max(1, H - SH2)));
-    auto emit_p2 = [&](int y) {
-        int16_t* orow = out + ((size_t)(y - a.out_row0) * W1) * D;
+    // output addressing: uniform row base + per-lane byte offset; the wave's column count and
+    // the active-lane predicate are hoisted so each row is one exec region of plain stores
+    const int ncols = min(CW, W1 - wx0);
+    const size_t colstride = (size_t)D * 2;
+    auto row_base = [&](int y) {
+        return (char*)(out + ((size_t)(y - a.out_row0) * W1 + wx0) * D) + 4 * lane;
+    };
+    auto emit = [&](int y, auto&& val) __attribute__((always_inline)) {
+        char* rb = row_base(y);
 #pragma unroll
-        for (int c = 0; c < CW; c++) {
-            const int x = wx0 + c;
-            if (x >= W1) continue;
+        for (int i = 0; i < K; i++) {
+            if (2 * (lane + 64 * i) < D) {
 #pragma unroll
-            for (int i = 0; i < K; i++) {
-                const int qp = lane + 64 * i;
-                if (2 * qp < D) *(uint32_t*)(orow + (size_t)x * D + 2 * qp) = P2x2;
+                for (int c = 0; c < CW; c++)
+                    if (c < ncols) *(uint32_t*)(rb + c * colstride + 256 * i) = val(i, c);
             }
         }
     };
+
+    // rows [yl, ty1) of MODE_HH keep the initial P2
+    int yl = ty1;
+    if (a.hh_bottom) yl = max(ty0, min(ty1, max(1, H - SH2)));
+    auto emit_p2 = [&](int y) { emit(y, [&](int, int) { return P2x2; }); };
     for (int y = yl; y < ty1; y++) emit_p2(y);
     if (yl <= ty0) return;
 
-    // staged column spans (matched index m -> image column minX1 + m)
-    const int mlo = min(max(bx0 - SW2, 0), W1 - 1);
-    const int mhi = min(max(bx0 + BCOLS + SW2 - 1, 0), W1 - 1);
-    const int NL = mhi - mlo + 1;
-    const int xr_lo = mlo + g.minX1 - g.minD - (D - 2);
-    const int NRP = NL + D - 2;
+    // Staged spans in VIRTUAL columns v = bx0 - SW2 + e (e = 0 .. NLV-1): L at image column
+    // minX1 + clamp(v); R pairs for xr = minX1 + v - minD - (D-2) + e', e' = 0 .. NLV+D-3, the
+    // right image's pair of disparities (2qp, 2qp+1) of column v at e' = (v - vlo) + D-2 - 2qp.
+    // Sources are clamped into the image; columns a wave sees beyond [0, W1) are then replaced
+    // by the edge column's pixel cost (clamp_edges), which is what x clamping means.
+    const int vlo = bx0 - SW2;
+    const int NRP = NLV + D - 2;
     const int STR = BCOLS + 2 * SW2 + D;
     const int HR = cost_half_r(STR);  // entries per parity half of a staged R plane
     const int BUF = 3 * STR + 6 * HR;
@@ -177,57 +214,56 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     const size_t plane = (size_t)H * W;
 
     // ---- staging: rows of the L splat planes and R pair planes into LDS buffer b ----
-    constexpr int NPR = 2;  // R entries per thread per plane (NRP <= 512)
-    uint64_t ql[3] = {0, 0, 0}, qr[3][NPR];
-    auto fetch = [&](int r) {
-        const size_t ro = (size_t)r * W;
-        if (tid < NL) {
+    // Loads are unconditional with clamped indices (surplus lanes re-load and re-store the last
+    // entry, the same value to the same slot): a guarded load makes hipcc branch around it and
+    // wait vmcnt(0) right after the prefetch is issued, exposing the full HBM latency per row.
+    constexpr int NPR = K;  // R entries per thread per plane: NRP <= 256 * K
+    const int il = min(tid, NLV - 1);
+    const int gl = g.minX1 + min(max(vlo + il, 0), W1 - 1);
+    const int xr0 = g.minX1 + vlo - g.minD - (D - 2);
+    int gr[NPR], pr[NPR];
 #pragma unroll
-            for (int k = 0; k < 3; k++) ql[k] = PLf[k * plane + ro + g.minX1 + mlo + tid];
-        }
+    for (int t = 0; t < NPR; t++) {
+        const int ir = min(tid + 256 * t, NRP - 1);
+        gr[t] = min(max(xr0 + ir, 0), W - 1);
+        pr[t] = (ir & 1) * HR + (ir >> 1);
+    }
+    uint64_t ql[3], qr[3][NPR];
+    auto fetch = [&](int r) {
+        const uint64_t* prow = PLf + (size_t)r * W;
+        const uint64_t* rrow = PRf + (size_t)r * W;
+#pragma unroll
+        for (int k = 0; k < 3; k++) ql[k] = prow[k * plane + gl];
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
-            for (int t = 0; t < NPR; t++) {
-                const int i = tid + 256 * t;
-                qr[k][t] = i < NRP ? PRf[k * plane + ro + xr_lo + i] : 0ull;
-            }
+            for (int t = 0; t < NPR; t++) qr[k][t] = rrow[k * plane + gr[t]];
     };
     auto put = [&](int b) {
         uint64_t* B = lds + (size_t)b * BUF;
         uint64_t* BR = B + 3 * STR;
-        if (tid < NL) {
 #pragma unroll
-            for (int k = 0; k < 3; k++) B[k * STR + tid] = ql[k];
-        }
+        for (int k = 0; k < 3; k++) B[k * STR + il] = ql[k];
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
-            for (int t = 0; t < NPR; t++) {
-                const int i = tid + 256 * t;
-                if (i < NRP) BR[k * 2 * HR + (i & 1) * HR + (i >> 1)] = qr[k][t];
-            }
+            for (int t = 0; t < NPR; t++) BR[k * 2 * HR + pr[t]] = qr[k][t];
     };
 
-    // per-lane disparity pairs
-    int xoff[K];
+    // per-lane staged R position of column j: (j & 1) * HR + (wave*CW + j) / 2 + (D-2)/2 - qp
+    int rpos[K];
     bool act[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
         const int qp = lane + 64 * i;
         act[i] = 2 * qp < D;
-        // staged R index of xr = minX1 + m - minD - 2qp is (m - mlo) + (D - 2 - 2qp): same parity
-        // as m - mlo, position (parity half) + ((m - mlo) >> 1) + (D - 2) / 2 - qp
-        xoff[i] = act[i] ? (D - 2) / 2 - qp : 0;
+        rpos[i] = 3 * STR + wave * (CW / 2) + (act[i] ? (D - 2) / 2 - qp : 0);
     }
-    // per-column staged offsets (uniform, loop invariant)
-    int colL[NC], colR[NC];
-#pragma unroll
-    for (int j = 0; j < NC; j++) {
-        const int li = min(max(wx0 - SW2 + j, 0), W1 - 1) - mlo;
-        colL[j] = __builtin_amdgcn_readfirstlane(li);
-        colR[j] = __builtin_amdgcn_readfirstlane(3 * STR + (li & 1) * HR + (li >> 1));
-    }
+    const int lpos = wave * CW;
+    // block-edge waves: first / last in-image column among the wave's NC (NC = none)
+    const int j0 = max(0, -(wx0 - SW2));
+    const int j1 = min(NC - 1, W1 - 1 - (wx0 - SW2));
+    const bool edge = (j0 > 0) | (j1 < NC - 1);
 
     // virtual rows and outputs
     const int ylim = a.ylim, s0 = a.s0;
@@ -260,26 +296,26 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
             if (q + 2 <= qend) fetch(phys(q + 2));
         }
         const uint64_t* B = lds + (size_t)b * BUF;
+        const uint64_t* BL = B + lpos;
         // pixel costs of the NC columns of this wave, then the horizontal window sums
         uint32_t hs[K][CW];
         uint32_t pix[K][NC];
 #pragma unroll
         for (int j = 0; j < NC; j++) {
-            const int li = colL[j];
-            // broadcast LDS reads (every lane the same address): the L operands stay in VGPRs so
-            // several columns' loads can be in flight (no readfirstlane wait per column)
-            const uint64_t l0 = B[li], l1 = B[STR + li], l2 = B[2 * STR + li];
+            // broadcast LDS reads (every lane the same address) of the L operands
+            const uint64_t l0 = BL[j], l1 = BL[STR + j], l2 = BL[2 * STR + j];
             const uint32_t u = (uint32_t)l0, u0 = (uint32_t)(l0 >> 32), u1 = (uint32_t)l1;
             const uint32_t ur = (uint32_t)(l1 >> 32), ur0 = (uint32_t)l2, ur1 = (uint32_t)(l2 >> 32);
 #pragma unroll
             for (int i = 0; i < K; i++) {
-                const int xi = colR[j] + xoff[i];
-                const uint64_t r0 = B[xi], r1 = B[2 * HR + xi], r2 = B[4 * HR + xi];
+                const uint64_t* BRj = B + rpos[i] + (j & 1) * HR + (j >> 1);
+                const uint64_t r0 = BRj[0], r1 = BRj[2 * HR], r2 = BRj[4 * HR];
                 const uint32_t bs = bt_cost(u, u0, u1, (uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1);
                 const uint32_t br = bt_cost(ur, ur0, ur1, (uint32_t)(r1 >> 32), (uint32_t)r2, (uint32_t)(r2 >> 32));
-                pix[i][j] = pk_add(bs, as_u32(as_s16x2(br) >> (short)2));
+                pix[i][j] = pk_add(bs, pk_shr2_u(br));
             }
         }
+        if (edge) clamp_edges(pix, j0, j1, std::make_integer_sequence<int, NC>{});
 #pragma unroll
         for (int i = 0; i < K; i++) {
             uint32_t h = 0;
@@ -302,17 +338,7 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
             const int t = q - SH2;
             const int ya = (t == tlast) ? max(t, ty0) : t;
             const int yb = (t == tlast) ? yl : t + 1;
-            for (int y = ya; y < yb; y++) {
-                int16_t* orow = out + ((size_t)(y - a.out_row0) * W1) * D;
-#pragma unroll
-                for (int c = 0; c < CW; c++) {
-                    const int x = wx0 + c;
-                    if (x >= W1) continue;
-#pragma unroll
-                    for (int i = 0; i < K; i++)
-                        if (act[i]) *(uint32_t*)(orow + (size_t)x * D + 2 * (lane + 64 * i)) = pk_add(sum[i][c], P2x2);
-                }
-            }
+            for (int y = ya; y < yb; y++) emit(y, [&](int i, int c) { return pk_add(sum[i][c], P2x2); });
         }
         __syncthreads();
     };

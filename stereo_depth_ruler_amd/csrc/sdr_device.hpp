@@ -37,6 +37,20 @@ __device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
     return as_u32(__builtin_elementwise_max(as_s16x2(a), as_s16x2(b)));
 }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// unsigned saturating a - b per half (v_pk_sub_u16 clamp)
+__device__ __forceinline__ uint32_t pk_sub_usat(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_sub_sat(as_u16x2(a), as_u16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_max(as_u16x2(a), as_u16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_min(as_u16x2(a), as_u16x2(b)));
+}
+__device__ __forceinline__ uint32_t pk_shr2_u(uint32_t a) { return as_u32(as_u16x2(a) >> (unsigned short)2); }
 __device__ __forceinline__ uint32_t splat16(int v) {
     return (uint32_t)(v & 0xffff) * 0x00010001u;
 }
@@ -90,6 +104,14 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
     m = min((uint32_t)p16[0], (uint32_t)p16[1]);
     auto p32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
     return min((uint32_t)p32[0], (uint32_t)p32[1]);
+}
+
+// Unsigned 32-bit minimum over each 16-lane DPP row, broadcast within the row.
+__device__ __forceinline__ uint32_t row16_min_u32(uint32_t m) {
+    m = min(m, dpp_mov<kDppQuadXor1>(m));
+    m = min(m, dpp_mov<kDppQuadXor2>(m));
+    m = min(m, dpp_mov<kDppRowHalfMirror>(m));
+    return min(m, dpp_mov<kDppRowMirror>(m));
 }
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }

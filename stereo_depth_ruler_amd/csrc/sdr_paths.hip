@@ -31,8 +31,12 @@ __device__ __forceinline__ Regs<K> load_regs(const int16_t* p) {
         v.r[0] = t.x;
         v.r[1] = t.y;
     } else {
-        uint4 t = *(const uint4*)p;
-        v.r[0] = t.x; v.r[1] = t.y; v.r[2] = t.z; v.r[3] = t.w;
+        static_assert(K % 4 == 0, "K = 1, 2 or a multiple of 4");
+#pragma unroll
+        for (int j = 0; j < K / 4; j++) {
+            uint4 t = ((const uint4*)p)[j];
+            v.r[4 * j] = t.x; v.r[4 * j + 1] = t.y; v.r[4 * j + 2] = t.z; v.r[4 * j + 3] = t.w;
+        }
     }
     return v;
 }
@@ -44,7 +48,9 @@ __device__ __forceinline__ void store_regs(int16_t* p, const Regs<K>& v) {
     } else if constexpr (K == 2) {
         *(uint2*)p = make_uint2(v.r[0], v.r[1]);
     } else {
-        *(uint4*)p = make_uint4(v.r[0], v.r[1], v.r[2], v.r[3]);
+#pragma unroll
+        for (int j = 0; j < K / 4; j++)
+            ((uint4*)p)[j] = make_uint4(v.r[4 * j], v.r[4 * j + 1], v.r[4 * j + 2], v.r[4 * j + 3]);
     }
 }
 
@@ -172,20 +178,26 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 
 // ------------------------------------------------------------------------------------------
 // A.8 + A.9 fused: WTA / uniqueness / subpixel / disp2 / LR check, one workgroup per row.
+// A pixel's D path-cost sums live on a 16-lane DPP row (DPL disparities per lane), so one wave
+// instruction covers 4 pixels: each lane loads DPL*2 contiguous bytes per direction (16 B at
+// D = 128: a wave reads 1 KiB of consecutive pixels), and the argmin is a 4-step row reduction.
 // ------------------------------------------------------------------------------------------
-constexpr int kWtaWaves = 16;
-constexpr int kWtaPF = 2;
+constexpr int kWtaWaves = 4;   // 4 workgroups/CU at <= 128 VGPRs: 720 rows resident in one pass
+constexpr int kWtaGL = 16;     // lanes per pixel
+constexpr int kWtaPPW = 4;     // pixels per wave instruction
 
-template <int DPL, bool PAD>
+template <int DPL, bool PAD, int NP>
 __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a) {
     constexpr int K = DPL / 2;
+    // directions x pairs x in-flight iterations held in registers: keep the ring near 64 VGPRs
+    constexpr int PF = (NP * K <= 16) ? 4 : (NP * K <= 24 ? 3 : 2);
     extern __shared__ int wsm[];
     const int W = g.W, W1 = g.W1, D = g.D;
     uint32_t* keys = (uint32_t*)wsm;   // [W]
     int* disp2 = wsm + W;              // [W]
     int* drow = wsm + 2 * W;           // [W]
     const int y = blockIdx.x, f = blockIdx.y;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, gl = lane & (kWtaGL - 1), grp = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t kInit = 32767u << 16;
     const int invalid = (g.minD - 1) * 16;
@@ -195,48 +207,49 @@ __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a
     }
     __syncthreads();
 
-    const bool active = !PAD || lane * DPL < D;
-    const int loff = (PAD ? min(lane, D / DPL - 1) : lane) * DPL;
-    const size_t rowoff = (size_t)f * a.cs_fstride + (size_t)y * W1 * D + loff;
+    const bool active = !PAD || gl * DPL < D;
+    const int d0 = (PAD ? min(gl, D / DPL - 1) : gl) * DPL;  // padding lanes re-read the last word
+    const size_t rowoff = (size_t)f * a.cs_fstride + (size_t)y * W1 * D + d0;
     const bool check_uniq = a.uniq > 0 || !a.uniq_simd;
     const int uniq_simd = a.uniq_simd ? 1 : 0;
     const int lhs_scale = 100 - a.uniq;
     // trunc((double)n * inv100u) == n / (100-u) for 0 <= n < 2^22
     const double inv100u = 1.0 / (double)(100 - a.uniq) * (1.0 + 0x1p-40);
-    const int np = a.npaths;
-
-    auto load_px = [&](int x, Regs<K>* dst) __attribute__((always_inline)) {
-        const size_t o = rowoff + (size_t)min(x, W1 - 1) * D;
+    const int16_t* Lp[NP];
 #pragma unroll
-        for (int p = 0; p < kMaxPaths; p++)
-            if (p < np) dst[p] = load_regs<K>(a.L[p] + o);
+    for (int p = 0; p < NP; p++) Lp[p] = a.L[p] + rowoff;
+
+    // iteration t of this wave covers pixels xw(t) .. xw(t)+3, pixel xw(t)+grp on this lane
+    const int nit = (W1 + kWtaPPW * kWtaWaves - 1) / (kWtaPPW * kWtaWaves);
+    auto xw = [&](int t) { return (t * kWtaWaves + wave) * kWtaPPW; };
+    auto load_px = [&](int t, Regs<K>* dst) __attribute__((always_inline)) {
+        const size_t o = (size_t)min(xw(t) + grp, W1 - 1) * D;
+#pragma unroll
+        for (int p = 0; p < NP; p++) dst[p] = load_regs<K>(Lp[p] + o);
     };
 
-    Regs<K> ring[kWtaPF][kMaxPaths];
+    Regs<K> ring[PF][NP];
 #pragma unroll
-    for (int s = 0; s < kWtaPF; s++) load_px(wave + s * kWtaWaves, ring[s]);
+    for (int s = 0; s < PF; s++) load_px(s, ring[s]);
 
-    auto pixel = [&](const int x, auto sc) __attribute__((always_inline)) {
+    auto iter = [&](const int t, auto sc) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
-        Regs<K> St;
+        Regs<K> St = ring[s][0];
 #pragma unroll
-        for (int i = 0; i < K; i++) St.r[i] = ring[s][0].r[i];
+        for (int p = 1; p < NP; p++)
 #pragma unroll
-        for (int p = 1; p < kMaxPaths; p++)
-            if (p < np)
-#pragma unroll
-                for (int i = 0; i < K; i++) St.r[i] = pk_add_sat(St.r[i], ring[s][p].r[i]);
-        load_px(x + kWtaPF * kWtaWaves, ring[s]);
+            for (int i = 0; i < K; i++) St.r[i] = pk_add_sat(St.r[i], ring[s][p].r[i]);
+        load_px(t + PF, ring[s]);
+        const int x = xw(t) + grp;
         uint32_t key = 0xffffffffu;
 #pragma unroll
         for (int i = 0; i < K; i++) {
-            const uint32_t d = (uint32_t)(lane * DPL + 2 * i);
+            const uint32_t d = (uint32_t)(gl * DPL + 2 * i);
             const uint32_t lo = (uint32_t)((int)(short)(St.r[i] & 0xffff) + 32768);
             const uint32_t hi = (uint32_t)((int)(short)(St.r[i] >> 16) + 32768);
-            const uint32_t kk = min((lo << 16) | d, (hi << 16) | (d + 1));
-            key = min(key, active ? kk : 0xffffffffu);
+            key = min(key, min((lo << 16) | d, (hi << 16) | (d + 1)));
         }
-        key = __builtin_amdgcn_readfirstlane(wave_min_u32(key));
+        key = row16_min_u32(active ? key : 0xffffffffu);
         const int minS = (int)(key >> 16) - 32768;
         const int best = (int)(key & 0xffff);
         // uniqueness: reject if some d with |d-best| > 1 has S[d]*(100-u) < minS*100 (scalar
@@ -248,7 +261,7 @@ __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a
         for (int i = 0; i < K; i++) {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                const int d = lane * DPL + 2 * i + h;
+                const int d = gl * DPL + 2 * i + h;
                 const int v = (int)(short)(h ? (St.r[i] >> 16) : (St.r[i] & 0xffff));
                 const int cs = (v < thr16) & uniq_simd;
                 const int cc = (v * lhs_scale < rhs) & (uniq_simd ^ 1);
@@ -256,7 +269,7 @@ __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a
             }
         }
         bad &= (int)active & (int)check_uniq;
-        const bool reject = __ballot(bad != 0) != 0;
+        const bool reject = ((__ballot(bad != 0) >> (16 * grp)) & 0xffffull) != 0;
         // subpixel: d*16 + ((S[d-1]-S[d+1])*16 + den) / (2*den), C truncating division
         const int dm = max(best - 1, 0), dp = min(best + 1, D - 1);
         uint32_t wm = St.r[0], wp = St.r[0];
@@ -265,27 +278,22 @@ __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a
             if (((dm % DPL) >> 1) == i) wm = St.r[i];
             if (((dp % DPL) >> 1) == i) wp = St.r[i];
         }
-        const uint32_t am = __builtin_amdgcn_readlane(wm, dm / DPL);
-        const uint32_t ap = __builtin_amdgcn_readlane(wp, dp / DPL);
+        const uint32_t am = (uint32_t)__shfl((int)wm, grp * kWtaGL + dm / DPL);
+        const uint32_t ap = (uint32_t)__shfl((int)wp, grp * kWtaGL + dp / DPL);
         const int Sm = (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
         const int Sp = (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
         const int den = max(Sm + Sp - 2 * minS, 1);
         const int q = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
         const int d16 = best * 16 + (((0 < best) & (best < D - 1)) ? q : 0);
-        if (lane == 0 && !reject) {
+        if (gl == 0 && !reject && x < W1) {
             drow[x + g.minX1] = d16 + g.minD * 16;
             const int x2 = x + g.minX1 - best - g.minD;
             if (x2 >= 0 && x2 < W) atomicMin(&keys[x2], ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
         }
     };
-    {
-        int x = wave;
-        for (; x + (kWtaPF - 1) * kWtaWaves < W1; x += kWtaPF * kWtaWaves) {
-            pixel(x, std::integral_constant<int, 0>{});
-            pixel(x + kWtaWaves, std::integral_constant<int, 1>{});
-        }
-        if (x < W1) pixel(x, std::integral_constant<int, 0>{});
-    }
+    int t = 0;
+    for (; t + PF <= nit; t += PF) unroll_rows(iter, t, std::make_integer_sequence<int, PF>{});
+    unroll_rows_tail(iter, t, nit - 1, std::make_integer_sequence<int, PF - 1>{});
     __syncthreads();
     for (int x = threadIdx.x; x < W; x += blockDim.x) {
         const uint32_t k = keys[x];
@@ -309,16 +317,29 @@ __global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a
     }
 }
 
-void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st) {
+template <int DPL, bool PAD>
+static void launch_wta_np(const Geometry& g, const WtaArgs& a, int F, hipStream_t st) {
     dim3 grid(g.H, F);
     const size_t lds = (size_t)3 * g.W * 4;
     const dim3 block(64 * kWtaWaves);
-    if (g.D <= 128) {
-        if (g.D < 128) hipLaunchKernelGGL((k_wta_lr<2, true>), grid, block, lds, st, g, a);
-        else hipLaunchKernelGGL((k_wta_lr<2, false>), grid, block, lds, st, g, a);
+    switch (a.npaths) {
+    case 3: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 3>), grid, block, lds, st, g, a); break;
+    case 5: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 5>), grid, block, lds, st, g, a); break;
+    default: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 8>), grid, block, lds, st, g, a); break;
+    }
+}
+
+void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st) {
+    // DPL = disparities per lane so that a pixel fits one 16-lane row
+    if (g.D <= 64) {
+        if (g.D < 64) launch_wta_np<4, true>(g, a, F, st);
+        else launch_wta_np<4, false>(g, a, F, st);
+    } else if (g.D <= 128) {
+        if (g.D < 128) launch_wta_np<8, true>(g, a, F, st);
+        else launch_wta_np<8, false>(g, a, F, st);
     } else {
-        if (g.D < 256) hipLaunchKernelGGL((k_wta_lr<4, true>), grid, block, lds, st, g, a);
-        else hipLaunchKernelGGL((k_wta_lr<4, false>), grid, block, lds, st, g, a);
+        if (g.D < 256) launch_wta_np<16, true>(g, a, F, st);
+        else launch_wta_np<16, false>(g, a, F, st);
     }
 }
 

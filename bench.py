@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--streams", type=int, default=2, help="frames in flight (one matcher + stream each)")
+    ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
     a = ap.parse_args()
 
     import torch
@@ -130,32 +132,41 @@ def main():
     Ls, Rs = S.make_batch(nf, H, W, D, seed0=1000 * rank)
     Ld = torch.from_numpy(Ls).to(dev)
     Rd = torch.from_numpy(Rs).to(dev)
-    m = sdr.StereoSGBM.create(*args, device=dev.index)
-    disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
-    xyz = torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev)
+    # S in-flight frames: one matcher (own scratch) and one HIP stream per slot, frames issued
+    # round-robin, so one frame's compute-bound stages (cost volume, speckle CCL) overlap the
+    # next frame's bandwidth-bound ones (path aggregation, WTA) and the E/W chain tail
+    ns = max(1, a.streams)
+    ms = [sdr.StereoSGBM.create(*args, device=dev.index) for _ in range(ns)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2 * ns)]
+    xyz = [torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev) for _ in range(ns)]
+    m = ms[0]
     gather_bufs = None
     if world > 1 and rank == 0:  # RCCL has no int16: gather the disparity bytes
         gather_bufs = [[torch.empty(batch * H * W * 2, dtype=torch.uint8, device=dev) for _ in range(world)]
-                       for _ in range(2)]
-    pending = [None, None]
+                       for _ in range(2 * ns)]
+    pending = [None] * (2 * ns)
 
     def step(i):
         j = (i * batch) % (nf - batch + 1) if nf > batch else 0
-        slot = i & 1
+        k = i % ns
+        slot = i % (2 * ns)
         if pending[slot] is not None:
             pending[slot].wait()
             pending[slot] = None
-        m.compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot], xyz=xyz)
-        if world > 1:
-            pending[slot] = dist.gather(as_bytes(disp[slot]), gather_bufs[slot] if rank == 0 else None,
-                                        dst=0, async_op=True)
+        with torch.cuda.stream(streams[k]):
+            ms[k].compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot],
+                                    xyz=xyz[k])
+            if world > 1:
+                pending[slot] = dist.gather(as_bytes(disp[slot]), gather_bufs[slot] if rank == 0 else None,
+                                            dst=0, async_op=True)
 
     for i in range(a.warmup):
         step(i)
     for p in pending:
         if p is not None:
             p.wait()
-    pending = [None, None]
+    pending = [None] * (2 * ns)
     torch.cuda.synchronize()
     if not a.no_kernel_timing:
         m.enable_timing(2)
@@ -179,48 +190,73 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
+    w1 = W - max(args[0] + D, 0) + min(args[0], 0)
+    cells = batch * H * w1 * D
+    P = NPATHS[mode]
+
+    def kernel_report(mm):
+        """Per-kernel HIP-event times of matcher mm since its last reset -> (kernels, roofline)."""
+        per_kind = {name: mm.kernel_time(kind, reset=False) for name, kind in KERNEL_KINDS.items()}
+        all_ms, _ = mm.kernel_time(-1, reset=True)
+        kern = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
+                       "share": round(ms / all_ms, 4) if all_ms else None}
+                for name, (ms, c) in per_kind.items() if c}
+        tot_ms, cnt = per_kind["k_paths"]
+        frames_seen = per_kind["prefilter"][1]
+        if not cnt:
+            return kern, None
+        # k_paths: every direction reads C (2 B/cell) and writes its own L_r (2 B/cell)
+        bytes_per_launch = cells * 4 * P
+        avg_s = tot_ms / cnt / 1e3
+        achieved = bytes_per_launch / avg_s / 1e9
+        roof = {
+            "bound": "hbm",
+            "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> (all {P} path directions of a batch in one launch)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": load_traffic(f"{a.config}:k_paths"),
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "bytes_model": f"4*P*cells, P={P}, cells=batch*H*W1*D={cells}",
+            "avg_launch_us": round(avg_s * 1e6, 2),
+            "launches_timed": cnt,
+            "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
+        }
+        # whole pipeline against the canonical 2+6P B/cell model (cost write, path C read +
+        # L write, WTA L read), over the summed kernel time of one step
+        pipe_bytes = cells * (2 + 6 * P)
+        gpu_s = all_ms / 1e3 / max(1, frames_seen)
+        roof["pipeline"] = {
+            "algorithmic_bytes_per_step": pipe_bytes,
+            "kernel_time_per_step_us": round(gpu_s * 1e6, 1),
+            "achieved": round(pipe_bytes / gpu_s / 1e9, 1),
+            "frac": round(pipe_bytes / gpu_s / 1e9 / HBM_PEAK_GBS, 4),
+        }
+        return kern, roof
+
     roofline = None
     kernels = None
     if not a.no_kernel_timing:
-        per_kind = {name: m.kernel_time(kind, reset=False) for name, kind in KERNEL_KINDS.items()}
-        all_ms, all_cnt = m.kernel_time(-1, reset=True)
+        kernels, roofline = kernel_report(m)
+        if roofline is not None:
+            roofline["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
+                                    f"({ns} frames in flight: launches share the GPU with the other "
+                                    f"streams' kernels)")
+        if ns > 1 and roofline is not None:
+            # the same kernels with nothing beside them: a short single-stream segment after the
+            # timed region (kernel quality; the timed region's numbers include the overlap)
+            torch.cuda.synchronize()
+            m.kernel_time(-1, reset=True)
+            for i in range(a.iso_steps):
+                j = (i * batch) % (nf - batch + 1) if nf > batch else 0
+                m.compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[0], xyz=xyz[0])
+            torch.cuda.synchronize()
+            iso_k, iso_r = kernel_report(m)
+            iso_r["measured"] = f"HIP events, {a.iso_steps} single-stream steps after the timed region"
+            iso_r["kernels"] = iso_k
+            roofline["isolated"] = iso_r
         m.enable_timing(0)
-        tot_ms, cnt = per_kind["k_paths"]
-        w1 = W - max(args[0] + D, 0) + min(args[0], 0)
-        cells = batch * H * w1 * D
-        P = NPATHS[mode]
-        # k_paths: every direction reads C (2 B/cell) and writes its own L_r (2 B/cell)
-        bytes_per_launch = cells * 4 * P
-        kernels = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
-                          "share": round(ms / all_ms, 4) if all_ms else None}
-                   for name, (ms, c) in per_kind.items() if c}
-        if cnt:
-            avg_s = tot_ms / cnt / 1e3
-            achieved = bytes_per_launch / avg_s / 1e9
-            roofline = {
-                "bound": "hbm",
-                "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> (all {P} path directions of a batch in one launch)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": load_traffic(f"{a.config}:k_paths"),
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-                "bytes_model": f"4*P*cells, P={P}, cells=batch*H*W1*D={cells}",
-                "avg_launch_us": round(avg_s * 1e6, 2),
-                "launches_timed": cnt,
-                "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
-            }
-            # whole pipeline against the canonical 2+6P B/cell model (cost write, path C read +
-            # L write, WTA L read), over the summed kernel time of a step
-            pipe_bytes = cells * (2 + 6 * P)
-            gpu_s = all_ms / 1e3 / max(1, a.steps)
-            roofline["pipeline"] = {
-                "algorithmic_bytes_per_step": pipe_bytes,
-                "kernel_time_per_step_us": round(gpu_s * 1e6, 1),
-                "achieved": round(pipe_bytes / gpu_s / 1e9, 1),
-                "frac": round(pipe_bytes / gpu_s / 1e9 / HBM_PEAK_GBS, 4),
-            }
 
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6
@@ -245,6 +281,7 @@ def main():
                                 "disp12MaxDiff", "preFilterCap", "uniquenessRatio",
                                 "speckleWindowSize", "speckleRange", "mode"], args)),
             "parallelism": f"frame shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+            "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),
         "roofline": roofline,
@@ -258,7 +295,8 @@ def main():
             log("cpu baseline failed:", repr(e))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    m.close()
+    for mm in ms:
+        mm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

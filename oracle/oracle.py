@@ -28,10 +28,24 @@ class OrcParams(ctypes.Structure):
         "nstripes", "uniq_rule")]
 
 
+_SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "Makefile")
+
+
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(_LIB_PATH):
+    stale = not os.path.exists(_LIB_PATH) or any(
+        os.path.getmtime(os.path.join(_HERE, f)) > os.path.getmtime(_LIB_PATH) for f in _SOURCES)
+    if force or stale:
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return _LIB_PATH
+
+
+class WlsParams(ctypes.Structure):
+    """orc_wls_params (wls_oracle.h)."""
+    _fields_ = [("lambda_", ctypes.c_double), ("sigma_color", ctypes.c_double),
+                ("lrc_thresh", ctypes.c_int), ("depth_disc_radius", ctypes.c_int),
+                ("roll_off", ctypes.c_float), ("lambda_attenuation", ctypes.c_double),
+                ("num_iter", ctypes.c_int), ("roi_x", ctypes.c_int), ("roi_y", ctypes.c_int),
+                ("roi_w", ctypes.c_int), ("roi_h", ctypes.c_int), ("min_disp", ctypes.c_int)]
 
 
 def lib():
@@ -57,6 +71,14 @@ def lib():
         L.orc_bgr2gray.argtypes = [u8p, ci, ci, sz, u8p]
         L.orc_resize_area_half.argtypes = [u8p, ci, ci, sz, u8p]
         L.orc_disp_to_float.argtypes = [i16p, ci, f32p]
+        wp = ctypes.POINTER(WlsParams)
+        L.orc_wls_params_for_sgbm.argtypes = [ci, ci, ci, ci, ci, wp]
+        L.orc_fgs_lut.argtypes = [ctypes.c_double, f32p]
+        L.orc_wls_disc_map.argtypes = [i16p, ci, ci, ci, ci, ci, ci, ci, ctypes.c_float, f32p]
+        L.orc_wls_confidence.argtypes = [i16p, i16p, ci, ci, wp, f32p]
+        L.orc_fgs_filter_f32.argtypes = [u8p, sz, ci, ci, ctypes.c_double, ctypes.c_double,
+                                         ctypes.c_double, ci, f32p]
+        L.orc_wls_filter.argtypes = [i16p, i16p, u8p, sz, ci, ci, wp, i16p, f32p]
         _lib = L
     return _lib
 
@@ -160,3 +182,60 @@ def disp_to_float(disp: np.ndarray) -> np.ndarray:
     out = np.empty(disp.shape, np.float32)
     lib().orc_disp_to_float(_p(disp, ctypes.c_int16), disp.size, _p(out, ctypes.c_float))
     return out
+
+
+# ---- DisparityWLSFilter / FastGlobalSmootherFilter (wls_oracle.c) ----
+
+def wls_params_for_sgbm(minDisparity, numDisparities, blockSize, width, height, lambda_=8000.0,
+                        sigma_color=1.5) -> WlsParams:
+    p = WlsParams()
+    lib().orc_wls_params_for_sgbm(minDisparity, numDisparities, blockSize, width, height, ctypes.byref(p))
+    p.lambda_ = lambda_
+    p.sigma_color = sigma_color
+    return p
+
+
+def fgs_lut(sigma_color) -> np.ndarray:
+    out = np.empty(65026, np.float32)
+    lib().orc_fgs_lut(sigma_color, _p(out, ctypes.c_float))
+    return out
+
+
+def wls_disc_map(d, roi, radius, roll_off=0.001):
+    d = np.ascontiguousarray(d, np.int16)
+    h, w = d.shape
+    out = np.empty((h, w), np.float32)
+    lib().orc_wls_disc_map(_p(d, ctypes.c_int16), w, h, *roi, radius, roll_off, _p(out, ctypes.c_float))
+    return out
+
+
+def wls_confidence(dl, dr, p: WlsParams):
+    dl = np.ascontiguousarray(dl, np.int16)
+    dr = np.ascontiguousarray(dr, np.int16)
+    h, w = dl.shape
+    out = np.empty((h, w), np.float32)
+    lib().orc_wls_confidence(_p(dl, ctypes.c_int16), _p(dr, ctypes.c_int16), w, h, ctypes.byref(p),
+                             _p(out, ctypes.c_float))
+    return out
+
+
+def fgs_filter(guide, img, lambda_, sigma_color, attenuation=0.25, num_iter=3):
+    guide = np.ascontiguousarray(guide, np.uint8)
+    out = np.array(img, dtype=np.float32, copy=True, order="C")
+    h, w = out.shape
+    lib().orc_fgs_filter_f32(_p(guide, ctypes.c_uint8), guide.strides[0], w, h, lambda_, sigma_color,
+                             attenuation, num_iter, _p(out, ctypes.c_float))
+    return out
+
+
+def wls_filter(dl, dr, guide, p: WlsParams, return_conf=False):
+    dl = np.ascontiguousarray(dl, np.int16)
+    dr = np.ascontiguousarray(dr, np.int16)
+    guide = np.ascontiguousarray(guide, np.uint8)
+    h, w = dl.shape
+    out = np.empty((h, w), np.int16)
+    conf = np.empty((h, w), np.float32)
+    lib().orc_wls_filter(_p(dl, ctypes.c_int16), _p(dr, ctypes.c_int16), _p(guide, ctypes.c_uint8),
+                         guide.strides[0], w, h, ctypes.byref(p), _p(out, ctypes.c_int16),
+                         _p(conf, ctypes.c_float))
+    return (out, conf) if return_conf else out

@@ -3,7 +3,7 @@
 # usage: scripts/pmc_profile.sh <outdir> [bench args...]
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
-ARGS=${@:---steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing}
+ARGS=${@:---steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing --streams 1}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
 i=0

@@ -123,3 +123,98 @@ def reproject(disp, Q, handle_missing=False):
         m = float(disp.min())
         out[..., 2][np.abs(d - m) <= np.finfo(np.float32).eps] = 10000.0
     return out
+
+
+# ---- DisparityWLSFilter / FastGlobalSmootherFilter, float64 (independent of wls_oracle.c) ----
+
+def fgs_weights(guide, sigma):
+    """4-neighbour weights w = exp(-|dI|/sigma): (horizontal [h, w-1], vertical [h-1, w])."""
+    g = guide.astype(np.float64)
+    return np.exp(-np.abs(np.diff(g, axis=1)) / sigma), np.exp(-np.abs(np.diff(g, axis=0)) / sigma)
+
+
+def _solve_lines(f, wgt, lam):
+    """Rows of f: (I + lam * L_w) u = f with L_w the 1-D weighted path Laplacian (Neumann)."""
+    from scipy.linalg import solve_banded
+
+    n = f.shape[1]
+    out = np.empty_like(f)
+    for r in range(f.shape[0]):
+        w = wgt[r]
+        diag = np.ones(n)
+        diag[:-1] += lam * w
+        diag[1:] += lam * w
+        ab = np.zeros((3, n))
+        ab[0, 1:] = -lam * w
+        ab[1] = diag
+        ab[2, :-1] = -lam * w
+        out[r] = solve_banded((1, 1), ab, f[r])
+    return out
+
+
+def fgs_filter(guide, img, lam, sigma, attenuation=0.25, num_iter=3):
+    wh, wv = fgs_weights(guide, sigma)
+    u = img.astype(np.float64)
+    for _ in range(num_iter):
+        u = _solve_lines(u, wh, lam)
+        u = _solve_lines(u.T, wv.T, lam).T
+        lam *= attenuation
+    return u
+
+
+def _reflect101(idx, n):
+    if n == 1:
+        return np.zeros_like(idx)
+    idx = np.abs(idx)
+    period = 2 * n - 2
+    idx = idx % period
+    return np.where(idx >= n, period - idx, idx)
+
+
+def wls_disc_map(d, roi, radius, roll_off=0.001):
+    x, y, w, h = roi
+    out = np.ones(d.shape, np.float64)
+    if w <= 0 or h <= 0:
+        return out
+    sub = d[y:y + h, x:x + w].astype(np.float64)
+    rr = _reflect101(np.arange(-radius, h + radius), h)
+    cc = _reflect101(np.arange(-radius, w + radius), w)
+    pad = sub[rr][:, cc]
+    k = 2 * radius + 1
+    win = np.lib.stride_tricks.sliding_window_view(pad, (k, k))
+    mean = win.mean(axis=(-1, -2))
+    msq = (win ** 2).mean(axis=(-1, -2))
+    out[y:y + h, x:x + w] = np.maximum(1.0 - roll_off * (msq - mean ** 2), 0.0)
+    return out
+
+
+def wls_confidence(dl, dr, roi, radius, lrc_thresh=24, roll_off=0.001):
+    x, y, w, h = roi
+    W = dl.shape[1]
+    rroi = (W - (x + w), y, w, h)
+    cl = wls_disc_map(dl, roi, radius, roll_off)
+    cr = wls_disc_map(dr, rroi, radius, roll_off)
+    conf = cl.copy()
+    rows = np.arange(dl.shape[0])[:, None]
+    cols = np.arange(x, x + w)[None, :]
+    lv = dl[:, x:x + w].astype(np.int64)
+    ridx = cols - (lv >> 4)
+    inr = (ridx >= rroi[0]) & (ridx < rroi[0] + rroi[2])
+    rc = np.clip(ridx, 0, W - 1)
+    ok = np.abs(lv + dr[rows, rc].astype(np.int64)) < lrc_thresh
+    sub = conf[:, x:x + w]
+    sub[inr & ok] = np.minimum(cl[:, x:x + w], cr[rows, rc])[inr & ok]
+    sub[inr & ~ok] = 0.0
+    return 255.0 * conf
+
+
+def wls_filter(dl, dr, guide, roi, radius, lam, sigma, min_disp, lrc_thresh=24):
+    x, y, w, h = roi
+    conf = wls_confidence(dl, dr, roi, radius, lrc_thresh)
+    out = np.full(dl.shape, 16 * (min_disp - 1), np.float64)
+    c = conf[y:y + h, x:x + w]
+    g = guide[y:y + h, x:x + w]
+    num = fgs_filter(g, c * dl[y:y + h, x:x + w], lam, sigma)
+    den = fgs_filter(g, c, lam, sigma)
+    out[y:y + h, x:x + w] = np.where(den != 0, num / np.where(den != 0, den, 1), 0)
+    return out

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SDR_ABI_VERSION 1
+#define SDR_ABI_VERSION 2
 
 /* cv::StereoSGBM::MODE_* */
 enum { SDR_MODE_SGBM = 0, SDR_MODE_HH = 1, SDR_MODE_SGBM_3WAY = 2, SDR_MODE_HH4 = 3 };
@@ -73,6 +73,7 @@ typedef struct sdr_sgbm_params {
 } sdr_sgbm_params;
 
 typedef struct sdr_sgbm sdr_sgbm;
+typedef struct sdr_wls sdr_wls; /* ximgproc::DisparityWLSFilter (below) */
 
 /* StereoSGBM::create defaults: (0, 16, 3, 0, 0, 0, 0, 0, 0, 0, MODE_SGBM) */
 void sdr_sgbm_params_default(sdr_sgbm_params* p);
@@ -134,14 +135,60 @@ int sdr_resize_area_half_device(const uint8_t* d_src, int width, int height, siz
                                 uint8_t* d_dst, size_t dst_stride, int nframes, void* stream);
 
 /* StereoDisparity::computeDisparity class path (stereo_disparity.cpp:17-39) on host BGR frames:
- * cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left->compute(L, R) [-> right->compute(R, L)]
- * -> convertTo(CV_32F, 1/16), all on the left matcher's device.  out: float (height/2)x(width/2).
- * The ximgproc WLS filter (stereo_disparity.cpp:31) is not applied yet:
- * out is the left matcher's disparity; disp_left/disp_right (optional) receive the CV_16S maps. */
-int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr_left,
-                             const uint8_t* bgr_right, int width, int height, size_t bgr_stride,
-                             float* out, size_t out_stride, int16_t* disp_left,
-                             int16_t* disp_right);
+ * cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left->compute(L, R) -> right->compute(R, L)
+ * -> wls->filter(dl, left_small, filtered, dr) -> convertTo(CV_32F, 1/16), all on the left
+ * matcher's device.  out: float (height/2)x(width/2).  right and wls may be NULL (no WLS: out is
+ * the left matcher's disparity).  disp_left/disp_right/filtered (int16) and conf (float, the
+ * getConfidenceMap() of stereo_disparity.cpp:36) are optional host outputs of (h/2)x(w/2). */
+int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                             const uint8_t* bgr_left, const uint8_t* bgr_right, int width,
+                             int height, size_t bgr_stride, float* out, size_t out_stride,
+                             int16_t* disp_left, int16_t* disp_right, int16_t* filtered,
+                             float* conf);
+
+/* ---- ximgproc DisparityWLSFilter / FastGlobalSmootherFilter (class path, stereo_disparity.cpp:11-13,31,36) ----
+ * Field meaning follows opencv_contrib 4.6 ximgproc (disparity_filters.cpp, fgs_filter.cpp):
+ * the valid ROI of a W x H left map is (left_offset, top_offset, W-left-right, H-top-bottom). */
+typedef struct sdr_wls_params {
+    double lambda;                  /* setLambda (default 8000; the reference sets 8000) */
+    double sigma_color;             /* setSigmaColor (default 1.5; the reference sets 1.1) */
+    int lrc_thresh;                 /* setLRCthresh (24) */
+    int depth_discontinuity_radius; /* setDepthDiscontinuityRadius (SGBM: ceil(0.5*blockSize)) */
+    float roll_off;                 /* depth_discontinuity_roll_off_factor (0.001) */
+    double lambda_attenuation;      /* FGS lambda attenuation per iteration (0.25) */
+    int num_iter;                   /* FGS iterations (3) */
+    int left_offset, right_offset, top_offset, bottom_offset;
+    int min_disp;                   /* outside-ROI value is 16*(min_disp-1) */
+} sdr_wls_params;
+
+/* cv::ximgproc::createDisparityWLSFilter(matcher_left) (stereo_disparity.cpp:11): fills the
+ * filter parameters for an SGBM left matcher AND mutates the matcher's parameters the way
+ * ximgproc does (disp12MaxDiff = 1000000, speckleWindowSize = 0, uniquenessRatio = 0). */
+void sdr_wls_params_for_sgbm(sdr_sgbm_params* left_matcher, sdr_wls_params* out);
+int sdr_wls_create(const sdr_wls_params* p, int device, sdr_wls** out);
+int sdr_wls_destroy(sdr_wls* h);
+int sdr_wls_set_params(sdr_wls* h, const sdr_wls_params* p);
+int sdr_wls_get_params(const sdr_wls* h, sdr_wls_params* p);
+int sdr_wls_set_stream(sdr_wls* h, void* stream); /* NULL = the handle's own stream */
+void* sdr_wls_get_stream(const sdr_wls* h);
+/* DisparityWLSFilter::getROI for a W x H map: roi = {x, y, w, h}. */
+int sdr_wls_get_roi(const sdr_wls* h, int width, int height, int roi[4]);
+/* DisparityWLSFilter::filter(disp_left, left_view, filtered, disp_right) on device, async on the
+ * handle's stream: dense int16 maps [nframes][H][W], 8-bit gray guide (guide_stride bytes per
+ * row, guide_frame_stride bytes per frame) -> filtered int16 [nframes][H][W].  d_conf
+ * (nullable) receives getConfidenceMap() as float [nframes][H][W]. */
+int sdr_wls_filter_device(sdr_wls* h, const int16_t* d_disp_left, const int16_t* d_disp_right,
+                          const uint8_t* d_guide, int width, int height, size_t guide_stride,
+                          size_t guide_frame_stride, int nframes, int16_t* d_out, float* d_conf);
+/* Host-pointer version (synchronous). */
+int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_right,
+                   const uint8_t* guide, int width, int height, size_t guide_stride,
+                   int16_t* out, float* conf);
+/* cv::ximgproc::fastGlobalSmootherFilter(guide, src, dst, lambda, sigma, attenuation, iters) on
+ * nimg float images [nimg][h][w] sharing one 8-bit guide, in place, async on `stream`. */
+int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
+                          double lambda, double sigma_color, double lambda_attenuation,
+                          int num_iter, float* d_img, int nimg, void* stream);
 
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);

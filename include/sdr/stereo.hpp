@@ -5,6 +5,8 @@
 //   sdr::reprojectImageTo3D(disp, xyz, Q, handleMissing)    <- cv::reprojectImageTo3D
 //       stereo_disparity.cpp:78, pcd_write.cpp:116
 //   sdr::ximgproc::createRightMatcher(left)                 <- cv::ximgproc::createRightMatcher
+//   sdr::ximgproc::createDisparityWLSFilter(left)           <- cv::ximgproc::createDisparityWLSFilter
+//       stereo_disparity.cpp:10-13,31,36
 //   sdr::StereoDisparity                                     <- class StereoDisparity
 //       stereo_vision/include/stereo_disparity.hpp:8-24
 //
@@ -195,6 +197,58 @@ inline Ptr<StereoSGBM> createRightMatcher(const Ptr<StereoSGBM>& left) {
     sdr_right_matcher_params(&left->params(), &r);
     return StereoSGBM::create(r, left->device());
 }
+
+// cv::ximgproc::DisparityWLSFilter (stereo_disparity.cpp:11-13,31,36)
+class DisparityWLSFilter {
+public:
+    DisparityWLSFilter(const sdr_wls_params& p, int device) : p_(p) { check(sdr_wls_create(&p_, device, &h_)); }
+    ~DisparityWLSFilter() { sdr_wls_destroy(h_); }
+    DisparityWLSFilter(const DisparityWLSFilter&) = delete;
+    DisparityWLSFilter& operator=(const DisparityWLSFilter&) = delete;
+
+    double getLambda() const { return p_.lambda; }
+    void setLambda(double v) { p_.lambda = v; push(); }
+    double getSigmaColor() const { return p_.sigma_color; }
+    void setSigmaColor(double v) { p_.sigma_color = v; push(); }
+    int getLRCthresh() const { return p_.lrc_thresh; }
+    void setLRCthresh(int v) { p_.lrc_thresh = v; push(); }
+    int getDepthDiscontinuityRadius() const { return p_.depth_discontinuity_radius; }
+    void setDepthDiscontinuityRadius(int v) { p_.depth_discontinuity_radius = v; push(); }
+
+    // filter(disparity_map_left CV_16S, left_view CV_8UC1, filtered CV_16S, disparity_map_right CV_16S)
+    void filter(const Mat& dl, const Mat& left_view, Mat& filtered, const Mat& dr) {
+        if (dl.type != CV_16SC1 || dr.type != CV_16SC1 || dl.rows != dr.rows || dl.cols != dr.cols)
+            throw Exception(SDR_ERR_TYPE, "disparity maps must be CV_16S of equal size");
+        if (left_view.type != CV_8UC1 || left_view.rows != dl.rows || left_view.cols != dl.cols)
+            throw Exception(SDR_ERR_TYPE, "left_view must be CV_8UC1 of the disparity map's size");
+        if (dl.step != (size_t)dl.cols * 2 || dr.step != (size_t)dr.cols * 2)
+            throw Exception(SDR_ERR_ARG, "disparity maps must be continuous");
+        filtered.create(dl.rows, dl.cols, CV_16SC1);
+        conf_.create(dl.rows, dl.cols, CV_32FC1);
+        check(sdr_wls_filter(h_, dl.ptr<int16_t>(0), dr.ptr<int16_t>(0), left_view.data, dl.cols,
+                             dl.rows, left_view.step, filtered.ptr<int16_t>(0), conf_.ptr<float>(0)));
+    }
+    Mat getConfidenceMap() const { return conf_; }
+    sdr_wls* handle() const { return h_; }
+
+private:
+    void push() { check(sdr_wls_set_params(h_, &p_)); }
+    sdr_wls_params p_;
+    sdr_wls* h_ = nullptr;
+    Mat conf_;
+};
+
+// cv::ximgproc::createDisparityWLSFilter(matcher_left): also switches the left matcher to
+// disp12MaxDiff = 1e6, speckleWindowSize = 0, uniquenessRatio = 0, as ximgproc does
+inline Ptr<DisparityWLSFilter> createDisparityWLSFilter(const Ptr<StereoSGBM>& left) {
+    sdr_sgbm_params m = left->params();
+    sdr_wls_params p;
+    sdr_wls_params_for_sgbm(&m, &p);
+    left->setDisp12MaxDiff(m.disp12MaxDiff);
+    left->setSpeckleWindowSize(m.speckleWindowSize);
+    left->setUniquenessRatio(m.uniquenessRatio);
+    return Ptr<DisparityWLSFilter>(new DisparityWLSFilter(p, left->device()));
+}
 }  // namespace ximgproc
 
 // class StereoDisparity (reference stereo_vision/include/stereo_disparity.hpp:8-24)
@@ -205,9 +259,9 @@ public:
         matcher = StereoSGBM::create(0, 80, 5, 8 * 5 * 5 * 3, 32 * 5 * 5 * 3, 1, 63, 12, 200, 2,
                                      StereoSGBM::MODE_SGBM_3WAY, device);
         right_matcher = ximgproc::createRightMatcher(matcher);          // :10
-        // createDisparityWLSFilter(matcher) mutates the left matcher (:11)
-        matcher->setDisp12MaxDiff(1000000);
-        matcher->setSpeckleWindowSize(0);
+        wls_filter = ximgproc::createDisparityWLSFilter(matcher);       // :11
+        wls_filter->setLambda(8000.0);                                   // :12
+        wls_filter->setSigmaColor(1.1);                                  // :13
     }
     // BGR 8UC3 rectified pair (full res) -> CV_32F disparity in px at half resolution
     Mat computeDisparity(const Mat& left, const Mat& right) {
@@ -215,9 +269,11 @@ public:
             left.cols != right.cols || left.step != right.step)
             throw Exception(SDR_ERR_TYPE, "computeDisparity expects two equal-size BGR images");
         Mat out(left.rows / 2, left.cols / 2, CV_32FC1);
-        check(sdr_stereo_class_compute(matcher->handle(), right_matcher->handle(), left.data,
-                                       right.data, left.cols, left.rows, left.step,
-                                       out.ptr<float>(0), out.step / 4, nullptr, nullptr));
+        conf_map.create(left.rows / 2, left.cols / 2, CV_32FC1);
+        check(sdr_stereo_class_compute(matcher->handle(), right_matcher->handle(),
+                                       wls_filter->handle(), left.data, right.data, left.cols,
+                                       left.rows, left.step, out.ptr<float>(0), out.step / 4,
+                                       nullptr, nullptr, nullptr, conf_map.ptr<float>(0)));
         return out;
     }
     Mat computeDepth(const Mat& disparity) {  // stereo_disparity.cpp:76-80 (handleMissing=false)
@@ -226,10 +282,12 @@ public:
         return depth;
     }
     const Ptr<StereoSGBM> get_matcher() const { return matcher; }
+    const Mat& getConfidenceMap() const { return conf_map; }  // wls_filter->getConfidenceMap() (:36)
 
 private:
     Ptr<StereoSGBM> matcher, right_matcher;
-    Mat Q;
+    Ptr<ximgproc::DisparityWLSFilter> wls_filter;
+    Mat Q, conf_map;
 };
 
 }  // namespace sdr

@@ -83,8 +83,8 @@ void orc_wls_confidence(const int16_t* dl, const int16_t* dr, int W, int H, cons
     orc_wls_disc_map(dl, W, H, p->roi_x, p->roi_y, p->roi_w, p->roi_h, p->depth_disc_radius,
                      p->roll_off, conf);
     orc_wls_disc_map(dr, W, H, rrx, rry, rrw, rrh, p->depth_disc_radius, p->roll_off, rd);
-    /* ComputeDiscontinuityAwareLRC: every row, columns of the left ROI */
-    for (int i = 0; i < H; i++) {
+    /* ComputeDiscontinuityAwareLRC: rows and columns of the left ROI (stripes over its height) */
+    for (int i = p->roi_y; i < p->roi_y + p->roi_h; i++) {
         const int16_t* L = dl + (size_t)i * W;
         const int16_t* R = dr + (size_t)i * W;
         float* c = conf + (size_t)i * W;
@@ -144,8 +144,10 @@ void orc_fgs_filter_f32(const uint8_t* g, size_t gs, int w, int h, double lambda
     free(t);
 }
 
-/* saturate_cast<short>(float): round to nearest even, saturate */
+/* saturate_cast<short>(float) = saturate_cast<short>(cvRound(v)): round to nearest even; cvRound
+ * is cvtss2si, whose out-of-range/NaN result is INT_MIN (-> -32768 after saturation) */
 static int16_t sat_s16(float v) {
+    if (!(fabsf(v) < 2147483648.0f)) return -32768;
     const long r = lrintf(v);
     return (int16_t)(r < -32768 ? -32768 : (r > 32767 ? 32767 : r));
 }

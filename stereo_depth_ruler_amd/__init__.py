@@ -2,14 +2,19 @@
 Amar-Aliaga/Stereo_Depth_Ruler: cv::StereoSGBM::compute + cv::reprojectImageTo3D as hand-written
 HIP/CDNA4 kernels behind a C ABI (include/sdr/sdr.h), with an OpenCV-shaped Python surface.
 """
-from ._lib import SDRError, SgbmParams, LIB_PATH  # noqa: F401
+from ._lib import SDRError, SgbmParams, WlsParams, LIB_PATH  # noqa: F401
 from .sgbm import (  # noqa: F401
     MODE_HH, MODE_HH4, MODE_SGBM, MODE_SGBM_3WAY, StereoSGBM, createRightMatcher,
     cvt_bgr2gray, disparity_to_float, filterSpeckles, reprojectImageTo3D, resize_area_half,
 )
+from .ximgproc import (  # noqa: F401
+    DisparityWLSFilter, createDisparityWLSFilter, fastGlobalSmootherFilter,
+)
+from .stereo_disparity import StereoDisparity  # noqa: F401
 
 __all__ = [
     "SDRError", "SgbmParams", "StereoSGBM", "createRightMatcher", "reprojectImageTo3D",
     "disparity_to_float", "filterSpeckles", "cvt_bgr2gray", "resize_area_half",
-    "MODE_SGBM", "MODE_HH", "MODE_SGBM_3WAY", "MODE_HH4",
+    "MODE_SGBM", "MODE_HH", "MODE_SGBM_3WAY", "MODE_HH4", "WlsParams", "DisparityWLSFilter",
+    "createDisparityWLSFilter", "fastGlobalSmootherFilter", "StereoDisparity",
 ]

@@ -35,6 +35,16 @@ class SgbmParams(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class WlsParams(ctypes.Structure):
+    """sdr_wls_params (include/sdr/sdr.h)."""
+    _fields_ = [("lambda_", ctypes.c_double), ("sigma_color", ctypes.c_double),
+                ("lrc_thresh", ctypes.c_int), ("depth_discontinuity_radius", ctypes.c_int),
+                ("roll_off", ctypes.c_float), ("lambda_attenuation", ctypes.c_double),
+                ("num_iter", ctypes.c_int), ("left_offset", ctypes.c_int),
+                ("right_offset", ctypes.c_int), ("top_offset", ctypes.c_int),
+                ("bottom_offset", ctypes.c_int), ("min_disp", ctypes.c_int)]
+
+
 _lib = None
 
 # (name, restype, argtypes) for every function declared in include/sdr/sdr.h
@@ -65,7 +75,20 @@ SIGNATURES = [
     ("sdr_filter_speckles_device", _i, [_vp, _i, _i, _i, _i, _i, _i, _vp]),
     ("sdr_bgr2gray_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
     ("sdr_resize_area_half_device", _i, [_vp, _i, _i, _sz, _vp, _sz, _i, _vp]),
-    ("sdr_stereo_class_compute", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _sz, _vp, _vp]),
+    ("sdr_stereo_class_compute", _i,
+     [_vp, _vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("sdr_wls_params_for_sgbm", None, [_PP, _c.POINTER(WlsParams)]),
+    ("sdr_wls_create", _i, [_c.POINTER(WlsParams), _i, _c.POINTER(_vp)]),
+    ("sdr_wls_destroy", _i, [_vp]),
+    ("sdr_wls_set_params", _i, [_vp, _c.POINTER(WlsParams)]),
+    ("sdr_wls_get_params", _i, [_vp, _c.POINTER(WlsParams)]),
+    ("sdr_wls_set_stream", _i, [_vp, _vp]),
+    ("sdr_wls_get_stream", _vp, [_vp]),
+    ("sdr_wls_get_roi", _i, [_vp, _i, _i, _c.POINTER(_c.c_int)]),
+    ("sdr_wls_filter_device", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _sz, _i, _vp, _vp]),
+    ("sdr_wls_filter", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _vp]),
+    ("sdr_fgs_filter_device", _i, [_vp, _sz, _i, _i, _c.c_double, _c.c_double, _c.c_double, _i,
+                                   _vp, _i, _vp]),
     ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),
     ("sdr_sgbm_enable_timing", _i, [_vp, _i]),
     ("sdr_sgbm_last_timing", _i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libsdr.so")
-SOURCES = ["sdr_cost.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_engine.hip"]
+SOURCES = ["sdr_cost.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_engine.hip"]
 HEADERS = ["sdr_device.hpp", "sdr_internal.hpp"]
 ARCH = os.environ.get("SDR_OFFLOAD_ARCH", "gfx950")
 
@@ -35,17 +35,32 @@ def _stale() -> bool:
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
+    """Compiles each HIP source to an object in parallel (relocatable device code is not needed:
+    every kernel is launched from the file that defines it), then links the shared library."""
     if not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include")]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
-    cmd += ["-o", OUT + ".tmp"]
+    objdir = os.path.join(os.path.dirname(OUT), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             "-Wall", "-Wno-unused-function", "-Wno-unused-result",
+             "-I", os.path.join(ROOT, "include")]
+    hipcc = _hipcc()
+    objs, procs = [], []
+    for f in SOURCES:
+        obj = os.path.join(objdir, f.replace(".hip", ".o"))
+        cmd = [hipcc, *flags, "-c", os.path.join(CSRC, f), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd)))
+        objs.append(obj)
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT + ".tmp"]
     if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+        print(" ".join(link))
+    subprocess.check_call(link)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -82,25 +82,8 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     return SDR_OK;
 }
 
-struct Buf {
-    void* p = nullptr;
-    size_t n = 0;
-};
-
-int ensure(Buf& b, size_t bytes) {
-    if (b.n >= bytes && b.p) return SDR_OK;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.n = 0;
-    if (bytes == 0) return SDR_OK;
-    hipError_t e = hipMalloc(&b.p, bytes);
-    if (e != hipSuccess) {
-        b.p = nullptr;
-        return fail(SDR_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
-    }
-    b.n = bytes;
-    return SDR_OK;
-}
+using sdr::Buf;
+using sdr::ensure;
 
 struct Stripe {
     int s0, end, out0, aux_rows, ylim;
@@ -128,13 +111,30 @@ void stripes_of(const Eff& e, std::vector<Stripe>* out) {
 
 }  // namespace
 
+int sdr::set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+int sdr::ensure(Buf& b, size_t bytes) {
+    if (b.n >= bytes && b.p) return SDR_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (bytes == 0) return SDR_OK;
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(SDR_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+    }
+    b.n = bytes;
+    return SDR_OK;
+}
+
 struct sdr_sgbm {
     sdr_sgbm_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
-    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_f;
+    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // per-kernel event pairs (timing level 2), harvested by sdr_sgbm_kernel_time
@@ -420,7 +420,8 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
-                   &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_f})
+                   &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
+                   &h->cls_conf})
         if (b->p) (void)hipFree(b->p);
     for (auto ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -667,14 +668,15 @@ int sdr_resize_area_half_device(const uint8_t* d_src, int W, int H, size_t strid
     return SDR_OK;
 }
 
-int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr_left,
-                             const uint8_t* bgr_right, int W, int H, size_t bgr_stride,
-                             float* out, size_t out_stride, int16_t* disp_left,
-                             int16_t* disp_right) {
+int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                             const uint8_t* bgr_left, const uint8_t* bgr_right, int W, int H,
+                             size_t bgr_stride, float* out, size_t out_stride, int16_t* disp_left,
+                             int16_t* disp_right, int16_t* filtered, float* conf) {
     if (!left || !bgr_left || !bgr_right || !out) return fail(SDR_ERR_ARG, "null argument");
     if (W <= 0 || H <= 0 || bgr_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "bad size/stride");
     if ((W & 1) || (H & 1)) return fail(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
     if (right && right->device != left->device) return fail(SDR_ERR_ARG, "matchers on different devices");
+    if (wls && !right) return fail(SDR_ERR_ARG, "the WLS filter needs the right matcher's disparity");
     const int w2 = W / 2, h2 = H / 2;
     if (out_stride < (size_t)w2) return fail(SDR_ERR_ARG, "out_stride < width/2");
     SDR_HIP(hipSetDevice(left->device));
@@ -686,13 +688,17 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr
     if ((rc = ensure(left->cls_small, 2 * px2))) return rc;
     if ((rc = ensure(left->cls_dl, px2 * 2))) return rc;
     if ((rc = ensure(left->cls_dr, px2 * 2))) return rc;
+    if ((rc = ensure(left->cls_wls, px2 * 2))) return rc;
     if ((rc = ensure(left->cls_f, px2 * 4))) return rc;
+    if ((rc = ensure(left->cls_conf, conf ? px2 * 4 : 0))) return rc;
     uint8_t* bgr = (uint8_t*)left->cls_bgr.p;
     uint8_t* gray = (uint8_t*)left->cls_gray.p;
     uint8_t* small = (uint8_t*)left->cls_small.p;
     int16_t* dl = (int16_t*)left->cls_dl.p;
     int16_t* dr = (int16_t*)left->cls_dr.p;
+    int16_t* dw = (int16_t*)left->cls_wls.p;
     float* f = (float*)left->cls_f.p;
+    float* dconf = conf ? (float*)left->cls_conf.p : nullptr;
     SDR_HIP(hipMemcpy2DAsync(bgr, (size_t)W * 3, bgr_left, bgr_stride, (size_t)W * 3, H, hipMemcpyHostToDevice, st));
     SDR_HIP(hipMemcpy2DAsync(bgr + px * 3, (size_t)W * 3, bgr_right, bgr_stride, (size_t)W * 3, H,
                              hipMemcpyHostToDevice, st));
@@ -701,24 +707,32 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, const uint8_t* bgr
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
     // matcher->compute(L, R) (stereo_disparity.cpp:27)
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, nullptr, nullptr, &fin))) return rc;
-    SDR_HIP(hipMemcpyAsync(dl, fin, px2 * 2, hipMemcpyDeviceToDevice, st));
+    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, dl, nullptr, &fin))) return rc;
     if (right) {
         // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
         hipStream_t rs = right->stream;
         right->stream = st;
-        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, nullptr, nullptr, &fin);
+        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, dr, nullptr, &fin);
         right->stream = rs;
         if (rc) return rc;
-        SDR_HIP(hipMemcpyAsync(dr, fin, px2 * 2, hipMemcpyDeviceToDevice, st));
     }
-    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34); WLS is not applied yet
-    sdr::launch_disp16_to_f32(dl, f, px2, st);
+    const int16_t* res = dl;
+    if (wls) {
+        // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)
+        void* ws = sdr_wls_get_stream(wls);
+        (void)sdr_wls_set_stream(wls, st);
+        rc = sdr_wls_filter_device(wls, dl, dr, small, w2, h2, w2, px2, 1, dw, dconf);
+        (void)sdr_wls_set_stream(wls, ws);
+        if (rc) return rc;
+        res = dw;
+    }
+    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34)
+    sdr::launch_disp16_to_f32(res, f, px2, st);
     SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
-    if (disp_left)
-        SDR_HIP(hipMemcpyAsync(disp_left, dl, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (disp_right && right)
-        SDR_HIP(hipMemcpyAsync(disp_right, dr, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, dl, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_right && right) SDR_HIP(hipMemcpyAsync(disp_right, dr, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (filtered) SDR_HIP(hipMemcpyAsync(filtered, res, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (conf && wls) SDR_HIP(hipMemcpyAsync(conf, dconf, px2 * 4, hipMemcpyDeviceToHost, st));
     SDR_HIP(hipStreamSynchronize(st));
     return SDR_OK;
 }

@@ -4,7 +4,18 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace sdr {
+
+// Device buffer that only grows (engine and WLS scratch); ensure() returns an SDR_* status.
+struct Buf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+int ensure(Buf& b, size_t bytes);
+// Records msg as the thread's sdr_last_error() and returns code.
+int set_error(int code, const std::string& msg);
 
 // Scanline directions of the path recurrence.
 enum Dir : int {

@@ -2,11 +2,8 @@
 stereo_vision/src/stereo_disparity.cpp), on the HIP engine.
 
 computeDisparity(left, right): BGR 8UC3 full-res rectified pair -> CV_32F half-res disparity (px):
-cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left SGBM (3WAY, d=80) and right matcher -> /16,
-all on the GPU (sdr_stereo_class_compute).  The ximgproc WLS filter of stereo_disparity.cpp:31 is
-the next row of the build and is not applied yet: the left matcher's disparity is
-returned, with the matcher already mutated the way createDisparityWLSFilter mutates it
-(disp12MaxDiff = 1e6, speckleWindowSize = 0).
+cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left SGBM (3WAY, d=80) and right matcher ->
+DisparityWLSFilter (lambda 8000, sigma 1.1) -> /16, all on the GPU (sdr_stereo_class_compute).
 computeDepth(disparity): reprojectImageTo3D(disparity, Q) (stereo_disparity.cpp:76-80), with the
 reference's quirk of a half-res disparity against the full-res Q kept as is.
 """
@@ -18,6 +15,7 @@ import numpy as np
 
 from ._lib import SDRError, check, lib
 from .sgbm import MODE_SGBM_3WAY, StereoSGBM, createRightMatcher, reprojectImageTo3D
+from .ximgproc import createDisparityWLSFilter
 
 
 class StereoDisparity:
@@ -27,11 +25,14 @@ class StereoDisparity:
         self.matcher = StereoSGBM.create(0, 80, 5, 8 * 5 * 5 * 3, 32 * 5 * 5 * 3, 1, 63, 12, 200, 2,
                                          MODE_SGBM_3WAY, device=device)
         self.right_matcher = createRightMatcher(self.matcher)  # :10
-        # createDisparityWLSFilter(matcher) (:11) mutates the left matcher [ximgproc]
-        self.matcher.setDisp12MaxDiff(1000000)
-        self.matcher.setSpeckleWindowSize(0)
+        # :11 -- also switches the left matcher to disp12MaxDiff 1e6, speckle 0, uniqueness 0
+        self.wls_filter = createDisparityWLSFilter(self.matcher)
+        self.wls_filter.setLambda(8000.0)  # :12
+        self.wls_filter.setSigmaColor(1.1)  # :13
         self.last_disp_left = None
         self.last_disp_right = None
+        self.last_filtered = None
+        self.conf_map = None
 
     def computeDisparity(self, left, right):
         left = np.ascontiguousarray(left, dtype=np.uint8)
@@ -42,10 +43,15 @@ class StereoDisparity:
         out = np.empty((h // 2, w // 2), np.float32)
         dl = np.empty((h // 2, w // 2), np.int16)
         dr = np.empty((h // 2, w // 2), np.int16)
-        check(lib().sdr_stereo_class_compute(self.matcher._h, self.right_matcher._h, left.ctypes.data,
+        fd = np.empty((h // 2, w // 2), np.int16)
+        conf = np.empty((h // 2, w // 2), np.float32)
+        check(lib().sdr_stereo_class_compute(self.matcher._h, self.right_matcher._h,
+                                             self.wls_filter._h, left.ctypes.data,
                                              right.ctypes.data, w, h, w * 3, out.ctypes.data, w // 2,
-                                             dl.ctypes.data, dr.ctypes.data))
-        self.last_disp_left, self.last_disp_right = dl, dr
+                                             dl.ctypes.data, dr.ctypes.data, fd.ctypes.data,
+                                             conf.ctypes.data))
+        self.last_disp_left, self.last_disp_right, self.last_filtered = dl, dr, fd
+        self.conf_map = conf  # wls_filter->getConfidenceMap() (:36)
         return out
 
     def computeDepth(self, disparity):

@@ -21,7 +21,7 @@ def declared_functions():
 
 
 def test_library_loads():
-    assert _lib.lib().sdr_abi_version() == 1
+    assert _lib.lib().sdr_abi_version() == 2
 
 
 def test_every_declared_symbol_exported():
@@ -100,3 +100,21 @@ def test_null_arguments_rejected():
     assert L.sdr_sgbm_compute(None, None, None, 8, 8, 1, 8, None, 8) == -1
     assert L.sdr_reproject(None, 8, 8, 8, None, 0, None, 24) == -1
     assert L.sdr_sgbm_set_params(None, None) == -1
+
+
+def test_wls_params_for_sgbm_matches_ximgproc(oracle):
+    """createDisparityWLSFilter(matcher): ROI offsets, radius, defaults, and the mutation of the
+    left matcher (disp12MaxDiff 1e6, speckle 0, uniqueness 0) -- host-only, no GPU."""
+    for minD, numD, bs, w, h in ((0, 80, 5, 640, 360), (-20, 64, 3, 300, 100), (5, 32, 7, 200, 50)):
+        m = _lib.SgbmParams(minD, numD, bs, 600, 2400, 1, 63, 12, 200, 2, 2, 4, 0)
+        p = _lib.WlsParams()
+        _lib.lib().sdr_wls_params_for_sgbm(ctypes.byref(m), ctypes.byref(p))
+        assert (m.disp12MaxDiff, m.speckleWindowSize, m.uniquenessRatio) == (1000000, 0, 0)
+        assert (m.minDisparity, m.numDisparities, m.blockSize, m.P1, m.P2) == (minD, numD, bs, 600, 2400)
+        q = oracle.wls_params_for_sgbm(minD, numD, bs, w, h)
+        assert (p.left_offset, p.top_offset) == (q.roi_x, q.roi_y)
+        assert w - p.left_offset - p.right_offset == q.roi_w and h - p.top_offset - p.bottom_offset == q.roi_h
+        assert p.depth_discontinuity_radius == q.depth_disc_radius
+        assert (p.lrc_thresh, p.num_iter, p.min_disp) == (q.lrc_thresh, q.num_iter, q.min_disp)
+        assert (p.lambda_, p.sigma_color, p.lambda_attenuation) == (q.lambda_, q.sigma_color, q.lambda_attenuation)
+        assert abs(p.roll_off - 0.001) < 1e-9

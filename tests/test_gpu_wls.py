@@ -1,0 +1,161 @@
+"""GPU parity of the class path's post-filter: ximgproc DisparityWLSFilter
++ FastGlobalSmootherFilter on the HIP engine against the CPU restatement (oracle/wls_oracle.c).
+
+The kernels evaluate every float operation in the oracle's order with contraction off, IEEE
+division and the oracle's host-computed weight table, so the filtered int16 map, the confidence
+map and raw FGS output are compared BIT FOR BIT.  Parity of the oracle itself against
+opencv_contrib is unpinned (no OpenCV in this image, no fixtures in the reference): see
+oracle/wls_oracle.h and tests/test_oracle_wls.py for how the restatement is pinned.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import stereo_depth_ruler_amd as sdr  # noqa: E402
+from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+from stereo_depth_ruler_amd.ximgproc import (  # noqa: E402
+    DisparityWLSFilter, createDisparityWLSFilter, fastGlobalSmootherFilter)
+from stereo_depth_ruler_amd._lib import WlsParams  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def wls_from_oracle_params(q) -> DisparityWLSFilter:
+    """A device filter with exactly the oracle's parameters (ROI given as offsets)."""
+    p = WlsParams(q.lambda_, q.sigma_color, q.lrc_thresh, q.depth_disc_radius, q.roll_off,
+                  q.lambda_attenuation, q.num_iter, q.roi_x, 0, q.roi_y, 0, q.min_disp)
+    return p
+
+
+def make_filter(q, W, H):
+    p = wls_from_oracle_params(q)
+    p.right_offset = W - q.roi_x - q.roi_w
+    p.bottom_offset = H - q.roi_y - q.roi_h
+    return DisparityWLSFilter(p)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 37), (29, 1), (40, 61), (64, 64), (65, 129),
+                                   (97, 130), (200, 333)])
+@pytest.mark.parametrize("lam,sigma", [(8000.0, 1.1), (50.0, 5.0)])
+def test_fgs_bit_exact(oracle, shape, lam, sigma):
+    rng = np.random.default_rng(sum(shape))
+    g = rng.integers(0, 256, shape).astype(np.uint8)
+    g[: shape[0] // 2] //= 8
+    x = (rng.random(shape) * 1000).astype(np.float32)
+    ref = oracle.fgs_filter(g, x, lam, sigma)
+    got = fastGlobalSmootherFilter(g, x, lam, sigma)
+    assert np.array_equal(bits(got), bits(ref))
+
+
+def test_fgs_stack_and_iterations(oracle):
+    rng = np.random.default_rng(5)
+    g = rng.integers(0, 256, (70, 90)).astype(np.uint8)
+    xs = (rng.random((3, 70, 90)) * 300).astype(np.float32)
+    got = fastGlobalSmootherFilter(g, xs, 8000.0, 1.1, 0.25, 5)
+    for i in range(3):
+        ref = oracle.fgs_filter(g, xs[i], 8000.0, 1.1, 0.25, 5)
+        assert np.array_equal(bits(got[i]), bits(ref))
+
+
+def sgbm_pair_maps(oracle, h, w, numD, seed, minD=0):
+    """Left / right disparity maps produced by the oracle SGBM on a synthetic pair, the way the
+    class path produces them (left matcher WLS-mutated, right matcher from createRightMatcher)."""
+    L, R, _ = S.make_pair(h, w, numD, seed=seed)
+    dl = oracle.sgbm_compute(L, R, oracle.make_params(minD, numD, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    dr = oracle.sgbm_compute(R, L, oracle.make_params(-(minD + numD) + 1, numD, 5, 600, 2400, 1000000,
+                                                      63, 0, 0, 2, 2))
+    return L, dl, dr
+
+
+@pytest.mark.parametrize("h,w,numD,seed", [(360, 640, 80, 1), (90, 200, 32, 2), (50, 121, 16, 3)])
+def test_wls_filter_bit_exact_on_sgbm_maps(oracle, h, w, numD, seed):
+    L, dl, dr = sgbm_pair_maps(oracle, h, w, numD, seed)
+    q = oracle.wls_params_for_sgbm(0, numD, 5, w, h, 8000.0, 1.1)
+    ref, ref_conf = oracle.wls_filter(dl, dr, L, q, return_conf=True)
+    f = make_filter(q, w, h)
+    got = f.filter(dl, L, dr)
+    assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf))
+    assert np.array_equal(got, ref)
+    assert f.getROI(w, h) == (q.roi_x, q.roi_y, q.roi_w, q.roi_h)
+
+
+def test_wls_params_variants(oracle):
+    """radius, LRC threshold, lambda/sigma, minDisparity < 0 (both ROI offsets), ROI y offsets."""
+    rng = np.random.default_rng(9)
+    h, w = 77, 190
+    base = rng.integers(2, 40, (h // 6 + 1, w // 6 + 1)) * 16
+    dl = np.repeat(np.repeat(base, 6, 0), 6, 1)[:h, :w].astype(np.int16)
+    dr = -np.roll(dl, -3, 1)
+    dl[rng.random((h, w)) < 0.05] = -16
+    g = rng.integers(0, 256, (h, w)).astype(np.uint8)
+    for (minD, numD, bs, lam, sig, thr) in ((0, 48, 5, 8000.0, 1.1, 24), (-10, 32, 3, 500.0, 3.0, 40),
+                                            (4, 16, 9, 8000.0, 1.5, 8)):
+        q = oracle.wls_params_for_sgbm(minD, numD, bs, w, h, lam, sig)
+        q.lrc_thresh = thr
+        q.roi_y, q.roi_h = 3, h - 7
+        ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)
+        f = make_filter(q, w, h)
+        got = f.filter(dl, g, dr)
+        assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf)), (minD, numD, bs)
+        assert np.array_equal(got, ref), (minD, numD, bs)
+
+
+def test_wls_edge_cases(oracle):
+    h, w = 40, 120
+    g = np.random.default_rng(1).integers(0, 256, (h, w)).astype(np.uint8)
+    cases = [
+        (np.full((h, w), 320, np.int16), np.full((h, w), -320, np.int16)),        # consistent
+        (np.full((h, w), 512, np.int16), np.full((h, w), 80, np.int16)),          # all LR fail -> 0
+        (np.full((h, w), -16, np.int16), np.full((h, w), -1280, np.int16)),       # all invalid
+        (np.random.default_rng(2).integers(-32768, 32767, (h, w)).astype(np.int16),
+         np.random.default_rng(3).integers(-32768, 32767, (h, w)).astype(np.int16)),  # extremes
+    ]
+    q = oracle.wls_params_for_sgbm(0, 32, 5, w, h, 8000.0, 1.1)
+    f = make_filter(q, w, h)
+    for dl, dr in cases:
+        ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)
+        got = f.filter(dl, g, dr)
+        assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf))
+        assert np.array_equal(got, ref)
+    # empty ROI (numDisparities >= width): everything is the fill value
+    q2 = oracle.wls_params_for_sgbm(0, 128, 5, w, h)
+    f2 = make_filter(q2, w, h)
+    got = f2.filter(cases[0][0], g, cases[0][1])
+    assert (got == -16).all()
+
+
+def test_wls_device_batch_equals_frames(oracle):
+    maps = [sgbm_pair_maps(oracle, 64, 160, 32, s) for s in (11, 12, 13)]
+    q = oracle.wls_params_for_sgbm(0, 32, 5, 160, 64, 8000.0, 1.1)
+    f = make_filter(q, 160, 64)
+    dev = torch.device("cuda", 0)
+    dl = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
+    dr = torch.from_numpy(np.stack([m[2] for m in maps])).to(dev)
+    g = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
+    out = f.filter(dl, g, dr)
+    torch.cuda.synchronize()
+    for i, (L, a, b) in enumerate(maps):
+        assert np.array_equal(out[i].cpu().numpy(), oracle.wls_filter(a, b, L, q))
+
+
+def test_create_wls_mutates_matcher():
+    m = sdr.StereoSGBM.create(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_SGBM_3WAY)
+    f = createDisparityWLSFilter(m)
+    assert (m.getDisp12MaxDiff(), m.getSpeckleWindowSize(), m.getUniquenessRatio()) == (1000000, 0, 0)
+    p = m.params()
+    assert (p.disp12MaxDiff, p.speckleWindowSize, p.uniquenessRatio) == (1000000, 0, 0)
+    f.setLambda(8000.0)
+    f.setSigmaColor(1.1)
+    assert f.getLambda() == 8000.0 and abs(f.getSigmaColor() - 1.1) < 1e-12
+    assert f.getDepthDiscontinuityRadius() == 3 and f.getROI(640, 360) == (80, 0, 560, 360)

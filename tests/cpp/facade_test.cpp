@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
         sdr::Mat BL = sdr::Mat::view(H, W, sdr::CV_8UC3, bl.data()), BR = sdr::Mat::view(H, W, sdr::CV_8UC3, br.data());
         sdr::Mat df = sd.computeDisparity(BL, BR);
         dump(out + "/class_disp.bin", df);
+        dump(out + "/class_conf.bin", sd.getConfidenceMap());
         sdr::Mat depth = sd.computeDepth(df);
         dump(out + "/class_depth.bin", depth);
         std::printf("numDisparities=%d\n", sd.get_matcher()->getNumDisparities());

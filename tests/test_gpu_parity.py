@@ -172,8 +172,22 @@ def test_reference_exact_class_matchers(oracle):
     assert np.array_equal(got_r, ref_r)
 
 
+def class_path_ref(oracle, bgr_l, bgr_r):
+    """Oracle composition of StereoDisparity::computeDisparity (stereo_disparity.cpp:17-39):
+    gray -> INTER_AREA 0.5 -> left matcher (3WAY d=80, mutated by createDisparityWLSFilter:
+    disp12MaxDiff 1e6, speckle 0, uniqueness 0) + right matcher -> WLS (8000, 1.1) -> /16."""
+    gl = oracle.resize_area_half(oracle.bgr2gray(bgr_l))
+    gr = oracle.resize_area_half(oracle.bgr2gray(bgr_r))
+    ref_l = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    ref_r = oracle.sgbm_compute(gr, gl, oracle.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    h, w = gl.shape
+    q = oracle.wls_params_for_sgbm(0, 80, 5, w, h, 8000.0, 1.1)
+    filt, conf = oracle.wls_filter(ref_l, ref_r, gl, q, return_conf=True)
+    return ref_l, ref_r, filt, conf, oracle.disp_to_float(filt)
+
+
 def test_class_path_stereo_disparity(oracle):
-    """StereoDisparity.computeDisparity: gray + INTER_AREA + left matcher + /16 on device."""
+    """StereoDisparity.computeDisparity: gray + INTER_AREA + both matchers + WLS + /16 on device."""
     from stereo_depth_ruler_amd.stereo_disparity import StereoDisparity
 
     rng = np.random.default_rng(7)
@@ -182,17 +196,17 @@ def test_class_path_stereo_disparity(oracle):
     bgr_r = np.stack([Rg, np.roll(Rg, 1, 1), rng.integers(0, 256, Rg.shape).astype(np.uint8)], -1)
     sd = StereoDisparity(S.REFERENCE_Q)
     out = sd.computeDisparity(bgr_l, bgr_r)
-    gl = oracle.resize_area_half(oracle.bgr2gray(bgr_l))
-    gr = oracle.resize_area_half(oracle.bgr2gray(bgr_r))
-    ref_l = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 12, 0, 2, 2))
-    ref_r = oracle.sgbm_compute(gr, gl, oracle.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    ref_l, ref_r, filt, conf, ref_out = class_path_ref(oracle, bgr_l, bgr_r)
     assert np.array_equal(sd.last_disp_left, ref_l)
     assert np.array_equal(sd.last_disp_right, ref_r)
-    assert np.array_equal(out, oracle.disp_to_float(ref_l))
+    assert np.array_equal(sd.conf_map.view(np.uint32), conf.view(np.uint32))
+    assert np.array_equal(sd.last_filtered, filt)
+    assert np.array_equal(out, ref_out)
     depth = sd.computeDepth(out)
     ref_depth = oracle.reproject(out, S.REFERENCE_Q, False)
     assert np.array_equal(depth.view(np.uint32), ref_depth.view(np.uint32))
     assert sd.get_matcher().getNumDisparities() == 80
+    assert sd.get_matcher().getUniquenessRatio() == 0
 
 
 def test_reproject_apis(oracle):
@@ -302,7 +316,7 @@ def test_cpp_facade(oracle, tmp_path):
     ref_xyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, True)
     assert np.array_equal(xyz.view(np.uint32), ref_xyz.view(np.uint32))
     cls = np.fromfile(tmp_path / "class_disp.bin", np.float32).reshape(H // 2, W // 2)
-    g = oracle.resize_area_half(L)
-    gr = oracle.resize_area_half(R)
-    ref_cls = oracle.sgbm_compute(g, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 12, 0, 2, 2))
-    assert np.array_equal(cls, oracle.disp_to_float(ref_cls))
+    _, _, _, conf, ref_cls = class_path_ref(oracle, bl, br)
+    assert np.array_equal(cls, ref_cls)
+    cconf = np.fromfile(tmp_path / "class_conf.bin", np.float32).reshape(H // 2, W // 2)
+    assert np.array_equal(cconf.view(np.uint32), conf.view(np.uint32))

@@ -14,6 +14,8 @@
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 
+#include <cstdlib>
+
 namespace sdr {
 
 template <int K>
@@ -39,6 +41,19 @@ __device__ __forceinline__ Regs<K> load_regs(const int16_t* p) {
         }
     }
     return v;
+}
+
+template <int K>
+__device__ __forceinline__ void store_regs_nt(int16_t* p, const Regs<K>& v) {
+    if constexpr (K == 1) {
+        __builtin_nontemporal_store(v.r[0], (uint32_t*)p);
+    } else if constexpr (K == 2) {
+        __builtin_nontemporal_store(v.r[0], (uint32_t*)p);
+        __builtin_nontemporal_store(v.r[1], (uint32_t*)p + 1);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K; j++) __builtin_nontemporal_store(v.r[j], (uint32_t*)p + j);
+    }
 }
 
 template <int K>
@@ -90,7 +105,7 @@ __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d,
     return ch;
 }
 
-template <int DPL, bool PAD>
+template <int DPL, bool PAD, bool NT = false>
 __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     constexpr int K = DPL / 2;
     constexpr int PF = 16;
@@ -156,23 +171,50 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
         m = wave_min_pk(m);
         delta2 = pk_add(m, P2x2);
         Lp = L;
-        if (k >= ch.kwrite && active) store_regs<K>(ob + (ptrdiff_t)k * pstep, L);
+        if (k >= ch.kwrite && active) {
+            if constexpr (NT) store_regs_nt<K>(ob + (ptrdiff_t)k * pstep, L);
+            else store_regs<K>(ob + (ptrdiff_t)k * pstep, L);
+        }
     };
     int k0 = 0;
     for (; k0 + PF <= ch.len; k0 += PF) unroll_rows(step, k0, std::make_integer_sequence<int, PF>{});
     unroll_rows_tail(step, k0, last, std::make_integer_sequence<int, PF - 1>{});
 }
 
-void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st) {
+static int exp_flag(const char* name) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : 0;
+}
+
+static void launch_paths_one(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st, bool nt) {
     const int total = pl.prefix[pl.ndirs];
     if (total <= 0) return;
     dim3 grid((total + 3) / 4, F);
     if (g.D <= 128) {
         if (g.D < 128) hipLaunchKernelGGL((k_paths<2, true>), grid, dim3(256), 0, st, g, pl);
+        else if (nt) hipLaunchKernelGGL((k_paths<2, false, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<2, false>), grid, dim3(256), 0, st, g, pl);
     } else {
         if (g.D < 256) hipLaunchKernelGGL((k_paths<4, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<4, false>), grid, dim3(256), 0, st, g, pl);
+    }
+}
+
+void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st) {
+    static const int nt = exp_flag("SDR_EXP_NT"), seq = exp_flag("SDR_EXP_SEQ");
+    if (!seq) return launch_paths_one(g, pl, F, st, nt);
+    // experiment: one launch per direction (3WAY stripes stay with their direction)
+    int i = 0;
+    while (i < pl.ndirs) {
+        int j = i + 1;
+        while (j < pl.ndirs && pl.d[j].dir == pl.d[i].dir) j++;
+        PathLaunch sub = pl;
+        sub.ndirs = j - i;
+        for (int k = i; k < j; k++) sub.d[k - i] = pl.d[k];
+        sub.prefix[0] = 0;
+        for (int k = 0; k < sub.ndirs; k++) sub.prefix[k + 1] = sub.prefix[k] + sub.d[k].nchains;
+        launch_paths_one(g, sub, F, st, nt);
+        i = j;
     }
 }
 

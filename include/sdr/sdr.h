@@ -169,7 +169,9 @@ int sdr_wls_create(const sdr_wls_params* p, int device, sdr_wls** out);
 int sdr_wls_destroy(sdr_wls* h);
 int sdr_wls_set_params(sdr_wls* h, const sdr_wls_params* p);
 int sdr_wls_get_params(const sdr_wls* h, sdr_wls_params* p);
-int sdr_wls_set_stream(sdr_wls* h, void* stream); /* NULL = the handle's own stream */
+/* HIP stream the filter launches on (NULL = the HIP null stream); reset = its own stream */
+int sdr_wls_set_stream(sdr_wls* h, void* stream);
+int sdr_wls_reset_stream(sdr_wls* h);
 void* sdr_wls_get_stream(const sdr_wls* h);
 /* DisparityWLSFilter::getROI for a W x H map: roi = {x, y, w, h}. */
 int sdr_wls_get_roi(const sdr_wls* h, int width, int height, int roi[4]);
@@ -189,6 +191,56 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_rig
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
                           double lambda, double sigma_color, double lambda_attenuation,
                           int num_iter, float* d_img, int nimg, void* stream);
+
+/* ---- ingest in front of the path: StereoRectifier + SBS split ----
+ * cv::initUndistortRectifyMap(K, dist, R, P, size, CV_16SC2, map1, map2)   stereo_rectifier.cpp:7-11
+ * computed on the device (f64, OpenCV's scalar loop): map1 int16 [H][W][2], map2 uint16 [H][W]
+ * (5-bit fractions, (v&31)*32 + (u&31)); host outputs.  dist has 0/4/5/8/12 coefficients; P is
+ * row-major 3 x p_cols (p_cols 3 or 4, only the first 3 columns are used). */
+int sdr_init_undistort_rectify_map(const double K[9], const double* dist, int ndist,
+                                   const double R[9], const double* P, int p_cols, int width,
+                                   int height, int device, int16_t* map1, uint16_t* map2);
+/* cv::remap(src, dst, map1, map2, INTER_LINEAR) with BORDER_CONSTANT 0 on 8-bit images with 1 or
+ * 3 channels, nframes frames (src/dst frame strides in bytes), async on `stream`. */
+int sdr_remap_bilinear_device(const uint8_t* d_src, int src_width, int src_height,
+                              size_t src_stride, size_t src_frame_stride, int channels,
+                              const int16_t* d_map1, const uint16_t* d_map2, int width, int height,
+                              uint8_t* d_dst, size_t dst_stride, size_t dst_frame_stride,
+                              int nframes, void* stream);
+
+typedef struct sdr_rectifier sdr_rectifier;
+/* StereoRectifier(config) (stereo_rectifier.cpp:6-11): both eyes' maps built on `device`. */
+int sdr_rectifier_create(const double K_left[9], const double* dist_left, int ndist_left,
+                         const double R1[9], const double* P1, const double K_right[9],
+                         const double* dist_right, int ndist_right, const double R2[9],
+                         const double* P2, int p_cols, int width, int height, int device,
+                         sdr_rectifier** out);
+int sdr_rectifier_destroy(sdr_rectifier* h);
+int sdr_rectifier_set_stream(sdr_rectifier* h, void* stream); /* NULL = the HIP null stream */
+int sdr_rectifier_reset_stream(sdr_rectifier* h);                /* back to its own stream */
+/* host copies of eye `which` (0 left, 1 right) maps */
+int sdr_rectifier_get_maps(const sdr_rectifier* h, int which, int16_t* map1, uint16_t* map2);
+/* StereoRectifier::rectify (stereo_rectifier.cpp:17-41) on device; either eye may be NULL. */
+int sdr_rectify_device(sdr_rectifier* h, const uint8_t* d_left, const uint8_t* d_right,
+                       size_t stride, size_t frame_stride, int channels, int nframes,
+                       uint8_t* d_left_out, uint8_t* d_right_out, size_t out_stride,
+                       size_t out_frame_stride);
+/* Side-by-side BGR frames [nframes] of (2*width) x height (stereo_displayer.cpp:155-159): split +
+ * rectify both eyes in one pass.  Outputs (each nullable, dense): rectified BGR [F][H][W][3] per
+ * eye, and/or the class path's input BGR2GRAY + INTER_AREA 0.5x of the rectified eye
+ * [F][H/2][W/2] (stereo_disparity.cpp:19-24), with OpenCV's intermediate u8 roundings. */
+int sdr_rectify_sbs_device(sdr_rectifier* h, const uint8_t* d_sbs, size_t sbs_stride,
+                           size_t sbs_frame_stride, int nframes, uint8_t* d_bgr_left,
+                           uint8_t* d_bgr_right, uint8_t* d_small_left, uint8_t* d_small_right);
+
+/* Class path from the half-size gray pair already on the device (after sdr_rectify_sbs_device),
+ * async on the left matcher's stream: left/right matchers (+ WLS when wls != NULL) for nframes
+ * dense [F][h][w] frames.  Outputs (device, dense): d_out float disparity in px (the value
+ * computeDisparity returns), d_filtered int16 (nullable), d_conf float (nullable). */
+int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                                    const uint8_t* d_small_left, const uint8_t* d_small_right,
+                                    int width, int height, int nframes, float* d_out,
+                                    int16_t* d_filtered, float* d_conf);
 
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);

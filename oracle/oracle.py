@@ -28,7 +28,8 @@ class OrcParams(ctypes.Structure):
         "nstripes", "uniq_rule")]
 
 
-_SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "Makefile")
+_SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "rectify_oracle.c",
+            "rectify_oracle.h", "Makefile")
 
 
 def build(force: bool = False) -> str:
@@ -79,6 +80,10 @@ def lib():
         L.orc_fgs_filter_f32.argtypes = [u8p, sz, ci, ci, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, ci, f32p]
         L.orc_wls_filter.argtypes = [i16p, i16p, u8p, sz, ci, ci, wp, i16p, f32p]
+        u16p = ctypes.POINTER(ctypes.c_uint16)
+        L.orc_rectify_inv_matrix.argtypes = [f64p, f64p, f64p, ci, f64p]
+        L.orc_init_undistort_rectify_map.argtypes = [f64p, f64p, ci, f64p, f64p, ci, ci, ci, i16p, u16p]
+        L.orc_remap_bilinear_u8.argtypes = [u8p, ci, ci, sz, ci, i16p, u16p, ci, ci, u8p, sz]
         _lib = L
     return _lib
 
@@ -239,3 +244,50 @@ def wls_filter(dl, dr, guide, p: WlsParams, return_conf=False):
                          guide.strides[0], w, h, ctypes.byref(p), _p(out, ctypes.c_int16),
                          _p(conf, ctypes.c_float))
     return (out, conf) if return_conf else out
+
+
+# ---- initUndistortRectifyMap / remap (rectify_oracle.c) ----
+
+def _f64(a, n):
+    a = np.ascontiguousarray(np.asarray(a, np.float64).reshape(-1))
+    assert a.size == n, (a.size, n)
+    return a
+
+
+def rectify_inv_matrix(K, R, P):
+    P = np.asarray(P, np.float64)
+    pc = P.shape[1] if P.ndim == 2 else (4 if P.size == 12 else 3)
+    K, R, P = _f64(K, 9), _f64(R, 9), _f64(P, 3 * pc)
+    out = np.empty(9, np.float64)
+    lib().orc_rectify_inv_matrix(_p(K, ctypes.c_double), _p(R, ctypes.c_double), _p(P, ctypes.c_double),
+                                 pc, _p(out, ctypes.c_double))
+    return out.reshape(3, 3)
+
+
+def init_undistort_rectify_map(K, dist, R, P, width, height):
+    """cv::initUndistortRectifyMap(K, dist, R, P, (width, height), CV_16SC2) -> (map1, map2)."""
+    P = np.asarray(P, np.float64)
+    pc = P.shape[1] if P.ndim == 2 else (4 if P.size == 12 else 3)
+    K, R, P = _f64(K, 9), _f64(R, 9), _f64(P, 3 * pc)
+    d = np.ascontiguousarray(np.asarray(dist, np.float64).reshape(-1))
+    m1 = np.empty((height, width, 2), np.int16)
+    m2 = np.empty((height, width), np.uint16)
+    lib().orc_init_undistort_rectify_map(_p(K, ctypes.c_double), _p(d, ctypes.c_double), d.size,
+                                         _p(R, ctypes.c_double), _p(P, ctypes.c_double), pc, width,
+                                         height, _p(m1, ctypes.c_int16), _p(m2, ctypes.c_uint16))
+    return m1, m2
+
+
+def remap_bilinear(src, map1, map2):
+    """cv::remap(src, dst, map1, map2, INTER_LINEAR) with BORDER_CONSTANT 0; src (H, W[, 3]) u8."""
+    src = np.ascontiguousarray(src, np.uint8)
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    sh, sw = src.shape[:2]
+    dh, dw = map2.shape
+    m1 = np.ascontiguousarray(map1, np.int16)
+    m2 = np.ascontiguousarray(map2, np.uint16)
+    out = np.empty((dh, dw) + (() if cn == 1 else (cn,)), np.uint8)
+    lib().orc_remap_bilinear_u8(_p(src, ctypes.c_uint8), sw, sh, src.strides[0], cn,
+                                _p(m1, ctypes.c_int16), _p(m2, ctypes.c_uint16), dw, dh,
+                                _p(out, ctypes.c_uint8), out.strides[0])
+    return out

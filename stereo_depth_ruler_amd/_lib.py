@@ -84,9 +84,25 @@ SIGNATURES = [
     ("sdr_wls_get_params", _i, [_vp, _c.POINTER(WlsParams)]),
     ("sdr_wls_set_stream", _i, [_vp, _vp]),
     ("sdr_wls_get_stream", _vp, [_vp]),
+    ("sdr_wls_reset_stream", _i, [_vp]),
+    ("sdr_rectifier_reset_stream", _i, [_vp]),
     ("sdr_wls_get_roi", _i, [_vp, _i, _i, _c.POINTER(_c.c_int)]),
     ("sdr_wls_filter_device", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _sz, _i, _vp, _vp]),
     ("sdr_wls_filter", _i, [_vp, _vp, _vp, _vp, _i, _i, _sz, _vp, _vp]),
+    ("sdr_init_undistort_rectify_map", _i,
+     [_c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _i, _c.POINTER(_c.c_double),
+      _c.POINTER(_c.c_double), _i, _i, _i, _i, _vp, _vp]),
+    ("sdr_remap_bilinear_device", _i, [_vp, _i, _i, _sz, _sz, _i, _vp, _vp, _i, _i, _vp, _sz, _sz, _i, _vp]),
+    ("sdr_rectifier_create", _i,
+     [_c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _i, _c.POINTER(_c.c_double),
+      _c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _i,
+      _c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _i, _i, _i, _i, _c.POINTER(_vp)]),
+    ("sdr_rectifier_destroy", _i, [_vp]),
+    ("sdr_rectifier_set_stream", _i, [_vp, _vp]),
+    ("sdr_rectifier_get_maps", _i, [_vp, _i, _vp, _vp]),
+    ("sdr_rectify_device", _i, [_vp, _vp, _vp, _sz, _sz, _i, _i, _vp, _vp, _sz, _sz]),
+    ("sdr_rectify_sbs_device", _i, [_vp, _vp, _sz, _sz, _i, _vp, _vp, _vp, _vp]),
+    ("sdr_stereo_class_compute_device", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     ("sdr_fgs_filter_device", _i, [_vp, _sz, _i, _i, _c.c_double, _c.c_double, _c.c_double, _i,
                                    _vp, _i, _vp]),
     ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),

@@ -134,7 +134,7 @@ struct sdr_sgbm {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
-    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf;
+    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // per-kernel event pairs (timing level 2), harvested by sdr_sgbm_kernel_time
@@ -421,7 +421,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
-                   &h->cls_conf})
+                   &h->cls_conf, &h->cls_filt})
         if (b->p) (void)hipFree(b->p);
     for (auto ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -668,6 +668,52 @@ int sdr_resize_area_half_device(const uint8_t* d_src, int W, int H, size_t strid
     return SDR_OK;
 }
 
+int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                                    const uint8_t* sl, const uint8_t* sr, int w2, int h2, int F,
+                                    float* d_out, int16_t* d_filtered, float* d_conf) {
+    if (!left || !sl || !sr || !d_out) return fail(SDR_ERR_ARG, "null argument");
+    if (w2 <= 0 || h2 <= 0 || F <= 0) return fail(SDR_ERR_ARG, "bad size");
+    if (right && right->device != left->device) return fail(SDR_ERR_ARG, "matchers on different devices");
+    if (wls && !right) return fail(SDR_ERR_ARG, "the WLS filter needs the right matcher's disparity");
+    SDR_HIP(hipSetDevice(left->device));
+    hipStream_t st = left->stream;
+    const size_t px2 = (size_t)w2 * h2;
+    int rc;
+    if ((rc = ensure(left->cls_dl, F * px2 * 2))) return rc;
+    if ((rc = ensure(left->cls_dr, F * px2 * 2))) return rc;
+    if ((rc = ensure(left->cls_wls, d_filtered ? 0 : F * px2 * 2))) return rc;
+    int16_t* dl = (int16_t*)left->cls_dl.p;
+    int16_t* dr = (int16_t*)left->cls_dr.p;
+    int16_t* dw = d_filtered ? d_filtered : (int16_t*)left->cls_wls.p;
+    // matcher->compute(L, R) (stereo_disparity.cpp:27)
+    int16_t* fin = nullptr;
+    if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
+    if (right) {
+        // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
+        hipStream_t rs = right->stream;
+        right->stream = st;
+        rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
+        right->stream = rs;
+        if (rc) return rc;
+    }
+    const int16_t* res = dl;
+    if (wls) {
+        // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)
+        void* ws = sdr_wls_get_stream(wls);
+        (void)sdr_wls_set_stream(wls, st);
+        rc = sdr_wls_filter_device(wls, dl, dr, sl, w2, h2, w2, px2, F, dw, d_conf);
+        (void)sdr_wls_set_stream(wls, ws);
+        if (rc) return rc;
+        res = dw;
+    } else if (d_filtered) {
+        SDR_HIP(hipMemcpyAsync(d_filtered, dl, F * px2 * 2, hipMemcpyDeviceToDevice, st));
+    }
+    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34)
+    sdr::launch_disp16_to_f32(res, d_out, F * px2, st);
+    SDR_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
 int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
                              const uint8_t* bgr_left, const uint8_t* bgr_right, int W, int H,
                              size_t bgr_stride, float* out, size_t out_stride, int16_t* disp_left,
@@ -675,8 +721,6 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     if (!left || !bgr_left || !bgr_right || !out) return fail(SDR_ERR_ARG, "null argument");
     if (W <= 0 || H <= 0 || bgr_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "bad size/stride");
     if ((W & 1) || (H & 1)) return fail(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
-    if (right && right->device != left->device) return fail(SDR_ERR_ARG, "matchers on different devices");
-    if (wls && !right) return fail(SDR_ERR_ARG, "the WLS filter needs the right matcher's disparity");
     const int w2 = W / 2, h2 = H / 2;
     if (out_stride < (size_t)w2) return fail(SDR_ERR_ARG, "out_stride < width/2");
     SDR_HIP(hipSetDevice(left->device));
@@ -686,18 +730,14 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     if ((rc = ensure(left->cls_bgr, 2 * px * 3))) return rc;
     if ((rc = ensure(left->cls_gray, 2 * px))) return rc;
     if ((rc = ensure(left->cls_small, 2 * px2))) return rc;
-    if ((rc = ensure(left->cls_dl, px2 * 2))) return rc;
-    if ((rc = ensure(left->cls_dr, px2 * 2))) return rc;
-    if ((rc = ensure(left->cls_wls, px2 * 2))) return rc;
     if ((rc = ensure(left->cls_f, px2 * 4))) return rc;
     if ((rc = ensure(left->cls_conf, conf ? px2 * 4 : 0))) return rc;
+    if ((rc = ensure(left->cls_filt, px2 * 2))) return rc;
     uint8_t* bgr = (uint8_t*)left->cls_bgr.p;
     uint8_t* gray = (uint8_t*)left->cls_gray.p;
     uint8_t* small = (uint8_t*)left->cls_small.p;
-    int16_t* dl = (int16_t*)left->cls_dl.p;
-    int16_t* dr = (int16_t*)left->cls_dr.p;
-    int16_t* dw = (int16_t*)left->cls_wls.p;
     float* f = (float*)left->cls_f.p;
+    int16_t* filt = (int16_t*)left->cls_filt.p;
     float* dconf = conf ? (float*)left->cls_conf.p : nullptr;
     SDR_HIP(hipMemcpy2DAsync(bgr, (size_t)W * 3, bgr_left, bgr_stride, (size_t)W * 3, H, hipMemcpyHostToDevice, st));
     SDR_HIP(hipMemcpy2DAsync(bgr + px * 3, (size_t)W * 3, bgr_right, bgr_stride, (size_t)W * 3, H,
@@ -705,33 +745,13 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     // cvtColor(BGR2GRAY) x2, resize(0.5, INTER_AREA) x2 (stereo_disparity.cpp:19-24)
     sdr::launch_bgr2gray(bgr, W, H, (size_t)W * 3, gray, W, 2, st);
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
-    // matcher->compute(L, R) (stereo_disparity.cpp:27)
-    int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(left, small, small + px2, w2, h2, w2, px2, 1, dl, nullptr, &fin))) return rc;
-    if (right) {
-        // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
-        hipStream_t rs = right->stream;
-        right->stream = st;
-        rc = enqueue_compute(right, small + px2, small, w2, h2, w2, px2, 1, dr, nullptr, &fin);
-        right->stream = rs;
-        if (rc) return rc;
-    }
-    const int16_t* res = dl;
-    if (wls) {
-        // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)
-        void* ws = sdr_wls_get_stream(wls);
-        (void)sdr_wls_set_stream(wls, st);
-        rc = sdr_wls_filter_device(wls, dl, dr, small, w2, h2, w2, px2, 1, dw, dconf);
-        (void)sdr_wls_set_stream(wls, ws);
-        if (rc) return rc;
-        res = dw;
-    }
-    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34)
-    sdr::launch_disp16_to_f32(res, f, px2, st);
+    if ((rc = sdr_stereo_class_compute_device(left, right, wls, small, small + px2, w2, h2, 1, f,
+                                              filt, dconf)))
+        return rc;
     SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
-    if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, dl, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (disp_right && right) SDR_HIP(hipMemcpyAsync(disp_right, dr, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (filtered) SDR_HIP(hipMemcpyAsync(filtered, res, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, left->cls_dl.p, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_right && right) SDR_HIP(hipMemcpyAsync(disp_right, left->cls_dr.p, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (filtered) SDR_HIP(hipMemcpyAsync(filtered, filt, px2 * 2, hipMemcpyDeviceToHost, st));
     if (conf && wls) SDR_HIP(hipMemcpyAsync(conf, dconf, px2 * 4, hipMemcpyDeviceToHost, st));
     SDR_HIP(hipStreamSynchronize(st));
     return SDR_OK;

@@ -433,7 +433,13 @@ int sdr_wls_get_params(const sdr_wls* h, sdr_wls_params* p) {
 
 int sdr_wls_set_stream(sdr_wls* h, void* stream) {
     if (!h) return sdr::set_error(SDR_ERR_ARG, "null handle");
-    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    h->stream = (hipStream_t)stream;  // NULL = the HIP null (legacy default) stream
+    return SDR_OK;
+}
+
+int sdr_wls_reset_stream(sdr_wls* h) {
+    if (!h) return sdr::set_error(SDR_ERR_ARG, "null handle");
+    h->stream = h->own_stream;
     return SDR_OK;
 }
 

@@ -218,3 +218,53 @@ def wls_filter(dl, dr, guide, roi, radius, lam, sigma, min_disp, lrc_thresh=24):
     den = fgs_filter(g, c, lam, sigma)
     out[y:y + h, x:x + w] = np.where(den != 0, num / np.where(den != 0, den, 1), 0)
     return out
+
+
+# ---- initUndistortRectifyMap / remap (independent vectorised restatement) ----
+
+def undistort_rectify_uv(K, dist, R, P):
+    """Per-pixel (u, v) source coordinates of cv::initUndistortRectifyMap in float64, with
+    x/y/w evaluated directly per pixel (OpenCV accumulates them along the row; the two agree to
+    a few ulp), returned as functions of the (H, W) grid."""
+    K = np.asarray(K, np.float64).reshape(3, 3)
+    R = np.asarray(R, np.float64).reshape(3, 3)
+    P = np.asarray(P, np.float64)
+    P = P.reshape(3, -1)[:, :3]
+    iR = np.linalg.inv(P @ R)
+    k = np.zeros(14)
+    d = np.asarray(dist, np.float64).reshape(-1)
+    k[:d.size] = d
+    k1, k2, p1, p2, k3, k4, k5, k6, s1, s2, s3, s4 = k[:12]
+
+    def uv(H, W):
+        i, j = np.mgrid[0:H, 0:W].astype(np.float64)
+        X = j * iR[0, 0] + i * iR[0, 1] + iR[0, 2]
+        Y = j * iR[1, 0] + i * iR[1, 1] + iR[1, 2]
+        Wh = j * iR[2, 0] + i * iR[2, 1] + iR[2, 2]
+        x, y = X / Wh, Y / Wh
+        r2 = x * x + y * y
+        kr = (1 + ((k3 * r2 + k2) * r2 + k1) * r2) / (1 + ((k6 * r2 + k5) * r2 + k4) * r2)
+        xd = x * kr + 2 * p1 * x * y + p2 * (r2 + 2 * x * x) + s1 * r2 + s2 * r2 * r2
+        yd = y * kr + p1 * (r2 + 2 * y * y) + 2 * p2 * x * y + s3 * r2 + s4 * r2 * r2
+        return K[0, 0] * xd + K[0, 2], K[1, 1] * yd + K[1, 2]
+    return uv
+
+
+def remap_bilinear(src, map1, map2):
+    """cv::remap INTER_LINEAR BORDER_CONSTANT(0) with CV_16SC2 maps, 8-bit, vectorised."""
+    src = np.asarray(src)
+    img = src[..., None] if src.ndim == 2 else src
+    H, W, C = img.shape
+    sx = map1[..., 0].astype(np.int64)
+    sy = map1[..., 1].astype(np.int64)
+    ax = (map2 & 31).astype(np.int64)
+    ay = (map2.astype(np.int64) >> 5) & 31
+    acc = np.zeros(map2.shape + (C,), np.int64)
+    for dy, dx, w in ((0, 0, (32 - ax) * (32 - ay)), (0, 1, ax * (32 - ay)),
+                      (1, 0, (32 - ax) * ay), (1, 1, ax * ay)):
+        xx, yy = sx + dx, sy + dy
+        ok = (xx >= 0) & (xx < W) & (yy >= 0) & (yy < H)
+        v = img[np.clip(yy, 0, H - 1), np.clip(xx, 0, W - 1)].astype(np.int64)
+        acc += np.where(ok[..., None], v, 0) * (w * 32)[..., None]
+    out = np.clip((acc + (1 << 14)) >> 15, 0, 255).astype(np.uint8)
+    return out[..., 0] if src.ndim == 2 else out

@@ -1,0 +1,159 @@
+"""GPU parity of the ingest step against oracle/rectify_oracle.c, BIT FOR BIT:
+rectification maps (cv::initUndistortRectifyMap CV_16SC2, computed on the device in f64 with
+contraction off), cv::remap INTER_LINEAR BORDER_CONSTANT (exact integer arithmetic), the fused
+side-by-side ingest (split -> rectify -> BGR2GRAY -> INTER_AREA 0.5x), and the reference's whole
+live-loop frame (stereo_displayer.cpp:155-162: SBS -> rectify -> StereoDisparity::computeDisparity
+-> computeDepth) as the device pipeline bench.py's C4 workload runs.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import stereo_depth_ruler_amd as sdr  # noqa: E402
+from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+from stereo_depth_ruler_amd.config import StereoConfiguration  # noqa: E402
+from stereo_depth_ruler_amd.rectify import StereoRectifier, initUndistortRectifyMap, remap  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.fixture(scope="module")
+def cfg():
+    c = StereoConfiguration()
+    assert c.loadFromFile(os.path.join(GOLDEN, "stereo.yaml"))
+    return c
+
+
+def test_maps_bit_exact_reference_calibration(oracle, cfg):
+    W, H = cfg.imageSize
+    r = StereoRectifier(cfg)
+    for eye, (K, D, R, P) in enumerate(((cfg.cameraMatrixLeft, cfg.distCoeffsLeft, cfg.R1, cfg.P1),
+                                        (cfg.cameraMatrixRight, cfg.distCoeffsRight, cfg.R2, cfg.P2))):
+        ref1, ref2 = oracle.init_undistort_rectify_map(K, D, R, P, W, H)
+        g1, g2 = r.maps(eye)
+        assert np.array_equal(g1, ref1) and np.array_equal(g2, ref2), f"eye {eye}"
+        h1, h2 = initUndistortRectifyMap(K, D, R, P, (W, H))
+        assert np.array_equal(h1, ref1) and np.array_equal(h2, ref2)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_maps_bit_exact_random_calibrations(oracle, seed):
+    rng = np.random.default_rng(seed)
+    W, H = int(rng.integers(50, 400)), int(rng.integers(40, 300))
+    f = rng.uniform(200, 900)
+    K = np.array([[f, 0, W / 2 + rng.normal(0, 10)], [0, f * rng.uniform(0.98, 1.02), H / 2 + rng.normal(0, 10)],
+                  [0, 0, 1]])
+    nd = [4, 5, 8, 12][seed % 4]
+    D = rng.normal(0, 0.05, nd)
+    a = rng.normal(0, 0.02, 3)
+    Rx = np.array([[1, 0, 0], [0, np.cos(a[0]), -np.sin(a[0])], [0, np.sin(a[0]), np.cos(a[0])]])
+    Ry = np.array([[np.cos(a[1]), 0, np.sin(a[1])], [0, 1, 0], [-np.sin(a[1]), 0, np.cos(a[1])]])
+    R = Rx @ Ry
+    P = np.hstack([K * rng.uniform(0.9, 1.1), rng.normal(0, 50, (3, 1))])
+    P[2] = [0, 0, 1, 0]
+    ref1, ref2 = oracle.init_undistort_rectify_map(K, D, R, P, W, H)
+    g1, g2 = initUndistortRectifyMap(K, D, R, P, (W, H))
+    assert np.array_equal(g1, ref1) and np.array_equal(g2, ref2)
+
+
+@pytest.mark.parametrize("cn", [1, 3])
+def test_remap_bit_exact(oracle, cn):
+    rng = np.random.default_rng(10 + cn)
+    sh, sw, dh, dw = 90, 130, 70, 150
+    img = rng.integers(0, 256, (sh, sw, 3) if cn == 3 else (sh, sw)).astype(np.uint8)
+    m1 = np.stack([rng.integers(-4, sw + 4, (dh, dw)), rng.integers(-4, sh + 4, (dh, dw))], -1).astype(np.int16)
+    m2 = rng.integers(0, 1024, (dh, dw)).astype(np.uint16)
+    assert np.array_equal(remap(img, m1, m2), oracle.remap_bilinear(img, m1, m2))
+
+
+def test_rectify_pair_bit_exact(oracle, cfg):
+    W, H = cfg.imageSize
+    rng = np.random.default_rng(4)
+    L = rng.integers(0, 256, (H, W, 3)).astype(np.uint8)
+    R = rng.integers(0, 256, (H, W, 3)).astype(np.uint8)
+    r = StereoRectifier(cfg)
+    lo, ro = r.rectify(L, R)
+    for eye, src, got in ((0, L, lo), (1, R, ro)):
+        m1, m2 = r.maps(eye)
+        assert np.array_equal(got, oracle.remap_bilinear(src, m1, m2))
+
+
+def sbs_frames(n, H=720, W=1280, seed=0):
+    """Synthetic ZED2-style side-by-side BGR frames: a seeded textured pair per frame."""
+    out = np.empty((n, H, 2 * W, 3), np.uint8)
+    rng = np.random.default_rng(seed)
+    for i in range(n):
+        Lg, Rg, _ = S.make_pair(H, W, 80, seed=seed + i)
+        out[i, :, :W] = np.stack([Lg, np.roll(Lg, 1, 1), rng.integers(0, 256, Lg.shape)], -1)
+        out[i, :, W:] = np.stack([Rg, np.roll(Rg, 1, 1), rng.integers(0, 256, Rg.shape)], -1)
+    return out
+
+
+def test_sbs_ingest_bit_exact(oracle, cfg):
+    W, H = cfg.imageSize
+    frames = sbs_frames(2, seed=20)
+    r = StereoRectifier(cfg)
+    out = r.rectify_sbs(frames)
+    for eye, key in ((0, "left"), (1, "right")):
+        m1, m2 = r.maps(eye)
+        for f in range(2):
+            half = frames[f, :, eye * W:(eye + 1) * W]
+            rect = oracle.remap_bilinear(half, m1, m2)
+            assert np.array_equal(out[key][f], rect)
+            small = oracle.resize_area_half(oracle.bgr2gray(rect))
+            assert np.array_equal(out["small_" + key][f], small)
+
+
+def test_live_loop_frame_device_pipeline(oracle, cfg):
+    """stereo_displayer.cpp:155-162 on the device: SBS -> rectify -> computeDisparity (gray, 0.5x,
+    left + right 3WAY d=80, WLS 8000/1.1, /16) -> computeDepth; checked against the oracle chain."""
+    from stereo_depth_ruler_amd.ximgproc import createDisparityWLSFilter
+    from stereo_depth_ruler_amd._lib import check, lib
+
+    W, H = cfg.imageSize
+    frames = sbs_frames(2, seed=30)
+    dev = torch.device("cuda", 0)
+    r = StereoRectifier(cfg)
+    small = r.rectify_sbs(torch.from_numpy(frames).to(dev), bgr=False)
+    left = sdr.StereoSGBM.create(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_SGBM_3WAY)
+    right = sdr.createRightMatcher(left)
+    wls = createDisparityWLSFilter(left)
+    wls.setLambda(8000.0)
+    wls.setSigmaColor(1.1)
+    F, h2, w2 = small["small_left"].shape
+    out = torch.empty((F, h2, w2), dtype=torch.float32, device=dev)
+    filt = torch.empty((F, h2, w2), dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream(0).cuda_stream
+    import ctypes
+    for h in (left._h,):
+        check(lib().sdr_sgbm_set_stream(h, ctypes.c_void_p(stream)))
+    check(lib().sdr_stereo_class_compute_device(left._h, right._h, wls._h, small["small_left"].data_ptr(),
+                                                small["small_right"].data_ptr(), w2, h2, F,
+                                                out.data_ptr(), filt.data_ptr(), None))
+    depth = sdr.reprojectImageTo3D(out, cfg.Q, False)
+    torch.cuda.synchronize()
+    for f in range(F):
+        ml, m2l = r.maps(0)
+        mr, m2r = r.maps(1)
+        gl = oracle.resize_area_half(oracle.bgr2gray(oracle.remap_bilinear(frames[f, :, :W], ml, m2l)))
+        gr = oracle.resize_area_half(oracle.bgr2gray(oracle.remap_bilinear(frames[f, :, W:], mr, m2r)))
+        dl = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+        dr = oracle.sgbm_compute(gr, gl, oracle.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+        q = oracle.wls_params_for_sgbm(0, 80, 5, w2, h2, 8000.0, 1.1)
+        fd = oracle.wls_filter(dl, dr, gl, q)
+        assert np.array_equal(filt[f].cpu().numpy(), fd)
+        df = oracle.disp_to_float(fd)
+        assert np.array_equal(out[f].cpu().numpy(), df)
+        ref_xyz = oracle.reproject(df, cfg.Q, False)
+        assert np.array_equal(depth[f].cpu().numpy().view(np.uint32), ref_xyz.view(np.uint32))

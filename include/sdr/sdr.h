@@ -242,6 +242,24 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
                                     int width, int height, int nframes, float* d_out,
                                     int16_t* d_filtered, float* d_conf);
 
+/* ---- point-cloud emit after the path, point_cloud/src/pcd_write.cpp ----
+ * Points are pcl::PointXYZRGB as savePCDFileBinary lays them out: 16-byte records
+ * {float x, y, z; uint32 rgba}. */
+/* convertCVMatToPCL(xyz, left) (pcd_write.cpp:17-51): xyz float [F][H][W][3], bgr u8 [F][H][W][3]
+ * or NULL -> organised cloud [F][H*W]; non-finite points get NaN x/y/z. Async on `stream`. */
+int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, int width, int height,
+                            int nframes, void* d_points, void* stream);
+/* pcl::VoxelGrid<PointXYZRGB> with leaf (lx, ly, lz) (pcd_write.cpp:122-130) on n device points
+ * -> d_out (capacity n) and *out_count.  PCL's int32-overflow case (leaf too small for the extent,
+ * the reference's 5 mm leaf on millimetre clouds) copies the input through and sets *passthrough.
+ * Synchronous on `stream` (the count is a host value). */
+int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float lz, void* d_out,
+                          int* out_count, int* passthrough, void* stream);
+/* pcl::io::savePCDFileBinary (pcd_write.cpp:141): header + width*height records (host memory).
+ * sdr_pcd_header returns the header length (writing it to buf when buf != NULL). */
+int sdr_pcd_header(int width, int height, char* buf, size_t cap);
+int sdr_write_pcd_binary(const char* path, const void* points, int width, int height);
+
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);
 

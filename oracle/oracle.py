@@ -29,7 +29,7 @@ class OrcParams(ctypes.Structure):
 
 
 _SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "rectify_oracle.c",
-            "rectify_oracle.h", "Makefile")
+            "rectify_oracle.h", "pcl_oracle.c", "pcl_oracle.h", "Makefile")
 
 
 def build(force: bool = False) -> str:
@@ -83,6 +83,10 @@ def lib():
         u16p = ctypes.POINTER(ctypes.c_uint16)
         L.orc_rectify_inv_matrix.argtypes = [f64p, f64p, f64p, ci, f64p]
         L.orc_init_undistort_rectify_map.argtypes = [f64p, f64p, ci, f64p, f64p, ci, ci, ci, i16p, u16p]
+        L.orc_xyz_to_cloud.argtypes = [f32p, u8p, ci, ci, f32p]
+        L.orc_voxel_grid.argtypes = [f32p, ci, ctypes.c_float, ctypes.c_float, ctypes.c_float, f32p,
+                                     ctypes.POINTER(ci)]
+        L.orc_voxel_grid.restype = ci
         L.orc_remap_bilinear_u8.argtypes = [u8p, ci, ci, sz, ci, i16p, u16p, ci, ci, u8p, sz]
         _lib = L
     return _lib
@@ -291,3 +295,27 @@ def remap_bilinear(src, map1, map2):
                                 _p(m1, ctypes.c_int16), _p(m2, ctypes.c_uint16), dw, dh,
                                 _p(out, ctypes.c_uint8), out.strides[0])
     return out
+
+
+# ---- convertCVMatToPCL / VoxelGrid (pcl_oracle.c) ----
+
+def xyz_to_cloud(xyz, bgr=None):
+    """convertCVMatToPCL(xyz CV_32FC3, left BGR) -> float32 (H*W, 4) {x, y, z, rgba bits}."""
+    xyz = np.ascontiguousarray(xyz, np.float32)
+    h, w, _ = xyz.shape
+    out = np.empty((h * w, 4), np.float32)
+    b = None if bgr is None else np.ascontiguousarray(bgr, np.uint8)
+    lib().orc_xyz_to_cloud(_p(xyz, ctypes.c_float), None if b is None else _p(b, ctypes.c_uint8), w, h,
+                           _p(out, ctypes.c_float))
+    return out
+
+
+def voxel_grid(points, leaf):
+    """pcl::VoxelGrid<PointXYZRGB>::filter -> (points (M, 4), passthrough flag)."""
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1, 4)
+    lx, ly, lz = (leaf, leaf, leaf) if np.isscalar(leaf) else leaf
+    out = np.empty_like(pts)
+    cnt = ctypes.c_int()
+    flag = lib().orc_voxel_grid(_p(pts, ctypes.c_float), pts.shape[0], lx, ly, lz, _p(out, ctypes.c_float),
+                                ctypes.byref(cnt))
+    return out[:cnt.value].copy(), bool(flag)

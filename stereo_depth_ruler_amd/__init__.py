@@ -7,6 +7,7 @@ from .sgbm import (  # noqa: F401
     MODE_HH, MODE_HH4, MODE_SGBM, MODE_SGBM_3WAY, StereoSGBM, createRightMatcher,
     cvt_bgr2gray, disparity_to_float, filterSpeckles, reprojectImageTo3D, resize_area_half,
 )
+from . import cloud  # noqa: F401
 from .ximgproc import (  # noqa: F401
     DisparityWLSFilter, createDisparityWLSFilter, fastGlobalSmootherFilter,
 )

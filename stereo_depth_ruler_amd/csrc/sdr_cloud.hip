@@ -1,0 +1,306 @@
+// sdr_cloud.hip -- the point-cloud emit after the hot path:
+//   convertCVMatToPCL(pointCloud_CV, left)       reference point_cloud/src/pcd_write.cpp:17-51,119
+//   pcl::VoxelGrid<PointXYZRGB>::filter          pcd_write.cpp:122-130
+//   pcl::io::savePCDFileBinary                   pcd_write.cpp:141
+// restating PCL 1.14 the way oracle/pcl_oracle.c does (the checker; parity with PCL unpinned).
+//
+// Points are PointXYZRGB as savePCDFileBinary lays them out: 16-byte records {x, y, z, rgba}.
+//   k_xyz_to_cloud   thread per pixel: 12 B XYZ + 3 B BGR in, 16 B out (HBM-bound, streaming)
+//   voxel grid       k_minmax (two-stage, exact float min/max over finite points) -> host decides
+//                    PCL's int32-overflow passthrough -> k_voxel_keys (64-bit key = voxel index <<
+//                    32 | point index, non-finite last) -> hipcub radix sort -> k_voxel_heads +
+//                    hipcub exclusive scan -> k_voxel_centroid (one thread per voxel sums its run in
+//                    point order: the oracle's order, so centroids match bit for bit)
+#include "../../include/sdr/sdr.h"
+#include "sdr_internal.hpp"
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace sdr {
+
+__device__ __forceinline__ bool finite3(float x, float y, float z) {
+    return isfinite(x) && isfinite(y) && isfinite(z);
+}
+
+__global__ __launch_bounds__(256) void k_xyz_to_cloud(const float* __restrict__ xyz,
+                                                      const uint8_t* __restrict__ bgr, size_t n,
+                                                      float4* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+        uint32_t rgba = 0xFF000000u;
+        float4 o;
+        if (finite3(x, y, z)) {
+            o.x = x;
+            o.y = y;
+            o.z = z;
+            if (bgr) rgba |= (uint32_t)bgr[3 * i + 2] << 16 | (uint32_t)bgr[3 * i + 1] << 8 | bgr[3 * i];
+        } else {
+            o.x = o.y = o.z = __uint_as_float(0x7FC00000u);
+        }
+        o.w = __uint_as_float(rgba);
+        out[i] = o;
+    }
+}
+
+constexpr int kMinMaxBlocks = 512;
+
+// partial[b] = {min x, y, z, max x, y, z, finite count (as float bits)}
+__global__ __launch_bounds__(256) void k_minmax(const float4* __restrict__ p, int n,
+                                                float* __restrict__ partial) {
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int cnt = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const float4 q = p[i];
+        if (!finite3(q.x, q.y, q.z)) continue;
+        cnt++;
+        mn[0] = fminf(mn[0], q.x); mn[1] = fminf(mn[1], q.y); mn[2] = fminf(mn[2], q.z);
+        mx[0] = fmaxf(mx[0], q.x); mx[1] = fmaxf(mx[1], q.y); mx[2] = fmaxf(mx[2], q.z);
+    }
+    __shared__ float s[7][256];
+    for (int c = 0; c < 3; c++) { s[c][threadIdx.x] = mn[c]; s[3 + c][threadIdx.x] = mx[c]; }
+    s[6][threadIdx.x] = __int_as_float(cnt);
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            for (int c = 0; c < 3; c++) {
+                s[c][threadIdx.x] = fminf(s[c][threadIdx.x], s[c][threadIdx.x + w]);
+                s[3 + c][threadIdx.x] = fmaxf(s[3 + c][threadIdx.x], s[3 + c][threadIdx.x + w]);
+            }
+            s[6][threadIdx.x] = __int_as_float(__float_as_int(s[6][threadIdx.x]) +
+                                               __float_as_int(s[6][threadIdx.x + w]));
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 7) partial[blockIdx.x * 7 + threadIdx.x] = s[threadIdx.x][0];
+}
+
+struct VoxelParams {
+    float inv[3];
+    int minb[3];
+    uint32_t mul1, mul2;
+};
+
+__global__ __launch_bounds__(256) void k_voxel_keys(const float4* __restrict__ p, int n, VoxelParams v,
+                                                    uint64_t* __restrict__ keys) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 q = p[i];
+    uint64_t k = ~0ull;
+    if (finite3(q.x, q.y, q.z)) {
+        const int i0 = (int)(floorf(q.x * v.inv[0]) - (float)v.minb[0]);
+        const int i1 = (int)(floorf(q.y * v.inv[1]) - (float)v.minb[1]);
+        const int i2 = (int)(floorf(q.z * v.inv[2]) - (float)v.minb[2]);
+        const uint32_t idx = (uint32_t)i0 + (uint32_t)i1 * v.mul1 + (uint32_t)i2 * v.mul2;
+        k = ((uint64_t)idx << 32) | (uint32_t)i;
+    }
+    keys[i] = k;
+}
+
+__global__ __launch_bounds__(256) void k_voxel_heads(const uint64_t* __restrict__ keys, int n,
+                                                     int* __restrict__ head) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    head[i] = k != ~0ull && (i == 0 || (keys[i - 1] >> 32) != (k >> 32)) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void k_voxel_centroid(const float4* __restrict__ p,
+                                                        const uint64_t* __restrict__ keys, int n,
+                                                        const int* __restrict__ head,
+                                                        const int* __restrict__ pos,
+                                                        float4* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || !head[i]) return;
+    const uint32_t idx = (uint32_t)(keys[i] >> 32);
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f, sa = 0.0f;
+    int j = i;
+    for (; j < n; j++) {
+        const uint64_t k = keys[j];
+        if (k == ~0ull || (uint32_t)(k >> 32) != idx) break;
+        const float4 q = p[(uint32_t)k];
+        const uint32_t c = __float_as_uint(q.w);
+        sx += q.x;
+        sy += q.y;
+        sz += q.z;
+        sr += (float)((c >> 16) & 255u);
+        sg += (float)((c >> 8) & 255u);
+        sb += (float)(c & 255u);
+        sa += (float)(c >> 24);
+    }
+    const float nn = (float)(j - i);
+    float4 o;
+    o.x = sx / nn;
+    o.y = sy / nn;
+    o.z = sz / nn;
+    o.w = __uint_as_float((uint32_t)(sa / nn) << 24 | (uint32_t)(sr / nn) << 16 |
+                          (uint32_t)(sg / nn) << 8 | (uint32_t)(sb / nn));
+    out[pos[i]] = o;
+}
+
+}  // namespace sdr
+
+namespace {
+
+#define CLOUD_HIP(call)                                                                          \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return sdr::set_error(SDR_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// stream-ordered scratch freed on every exit path
+struct AsyncScratch {
+    hipStream_t st;
+    std::vector<void*> ptrs;
+    explicit AsyncScratch(hipStream_t s) : st(s) {}
+    void* get(size_t bytes) {
+        void* p = nullptr;
+        if (hipMallocAsync(&p, bytes ? bytes : 1, st) != hipSuccess) return nullptr;
+        ptrs.push_back(p);
+        return p;
+    }
+    ~AsyncScratch() {
+        for (void* p : ptrs) (void)hipFreeAsync(p, st);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, int width, int height,
+                            int nframes, void* d_points, void* stream) {
+    if (!d_xyz || !d_points) return sdr::set_error(SDR_ERR_ARG, "null argument");
+    if (width <= 0 || height <= 0 || nframes <= 0) return sdr::set_error(SDR_ERR_ARG, "bad size");
+    const size_t n = (size_t)width * height * nframes;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(sdr::k_xyz_to_cloud, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_xyz,
+                       d_bgr, n, (float4*)d_points);
+    CLOUD_HIP(hipGetLastError());
+    return SDR_OK;
+}
+
+int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float lz, void* d_out,
+                          int* out_count, int* passthrough, void* stream) {
+    if (!d_points || !d_out || !out_count) return sdr::set_error(SDR_ERR_ARG, "null argument");
+    if (n < 0) return sdr::set_error(SDR_ERR_ARG, "negative point count");
+    if (!(lx > 0.0f) || !(ly > 0.0f) || !(lz > 0.0f)) return sdr::set_error(SDR_ERR_ARG, "leaf size must be > 0");
+    hipStream_t st = (hipStream_t)stream;
+    const float4* p = (const float4*)d_points;
+    float4* out = (float4*)d_out;
+    *out_count = 0;
+    if (passthrough) *passthrough = 0;
+    if (n == 0) return SDR_OK;
+    AsyncScratch scratch(st);
+    float* partial = (float*)scratch.get(sizeof(float) * 7 * sdr::kMinMaxBlocks);
+    if (!partial) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+    const int mmb = std::min(sdr::kMinMaxBlocks, (n + 255) / 256);
+    hipLaunchKernelGGL(sdr::k_minmax, dim3(mmb), dim3(256), 0, st, p, n, partial);
+    CLOUD_HIP(hipGetLastError());
+    std::vector<float> hp((size_t)7 * mmb);
+    CLOUD_HIP(hipMemcpyAsync(hp.data(), partial, sizeof(float) * hp.size(), hipMemcpyDeviceToHost, st));
+    CLOUD_HIP(hipStreamSynchronize(st));
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    long long nfin = 0;
+    for (int b = 0; b < mmb; b++) {
+        for (int c = 0; c < 3; c++) {
+            mn[c] = std::fmin(mn[c], hp[b * 7 + c]);
+            mx[c] = std::fmax(mx[c], hp[b * 7 + 3 + c]);
+        }
+        int cnt;
+        std::memcpy(&cnt, &hp[b * 7 + 6], 4);
+        nfin += cnt;
+    }
+    if (!nfin) return SDR_OK;  // nothing finite: empty output
+    const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
+    long long d[3];
+    for (int c = 0; c < 3; c++) d[c] = (long long)((mx[c] - mn[c]) * inv[c]) + 1;
+    const long long prod = (long long)((unsigned long long)d[0] * (unsigned long long)d[1] *
+                                       (unsigned long long)d[2]);
+    if (prod > 2147483647LL) {
+        // PCL: "Leaf size is too small for the input dataset. Integer indices would overflow." --
+        // the output is the input cloud unchanged
+        CLOUD_HIP(hipMemcpyAsync(out, p, sizeof(float4) * (size_t)n, hipMemcpyDeviceToDevice, st));
+        CLOUD_HIP(hipStreamSynchronize(st));
+        *out_count = n;
+        if (passthrough) *passthrough = 1;
+        return SDR_OK;
+    }
+    sdr::VoxelParams v;
+    int div[3];
+    for (int c = 0; c < 3; c++) {
+        v.inv[c] = inv[c];
+        v.minb[c] = (int)std::floor(mn[c] * inv[c]);
+        const int maxb = (int)std::floor(mx[c] * inv[c]);
+        div[c] = maxb - v.minb[c] + 1;
+    }
+    v.mul1 = (uint32_t)div[0];
+    v.mul2 = (uint32_t)div[0] * (uint32_t)div[1];
+    uint64_t* keys = (uint64_t*)scratch.get(sizeof(uint64_t) * n);
+    uint64_t* sorted = (uint64_t*)scratch.get(sizeof(uint64_t) * n);
+    int* head = (int*)scratch.get(sizeof(int) * n);
+    int* pos = (int*)scratch.get(sizeof(int) * n);
+    if (!keys || !sorted || !head || !pos) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+    const dim3 grid((n + 255) / 256);
+    hipLaunchKernelGGL(sdr::k_voxel_keys, grid, dim3(256), 0, st, p, n, v, keys);
+    size_t tb_sort = 0, tb_scan = 0;
+    CLOUD_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb_sort, keys, sorted, n, 0, 64, st));
+    CLOUD_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, head, pos, n, st));
+    void* tmp = scratch.get(std::max(tb_sort, tb_scan));
+    if (!tmp) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+    size_t tb = tb_sort;
+    CLOUD_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tb, keys, sorted, n, 0, 64, st));
+    hipLaunchKernelGGL(sdr::k_voxel_heads, grid, dim3(256), 0, st, sorted, n, head);
+    tb = tb_scan;
+    CLOUD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, head, pos, n, st));
+    hipLaunchKernelGGL(sdr::k_voxel_centroid, grid, dim3(256), 0, st, p, sorted, n, head, pos, out);
+    CLOUD_HIP(hipGetLastError());
+    int last_pos = 0, last_head = 0;
+    CLOUD_HIP(hipMemcpyAsync(&last_pos, pos + n - 1, 4, hipMemcpyDeviceToHost, st));
+    CLOUD_HIP(hipMemcpyAsync(&last_head, head + n - 1, 4, hipMemcpyDeviceToHost, st));
+    CLOUD_HIP(hipStreamSynchronize(st));
+    *out_count = last_pos + last_head;
+    return SDR_OK;
+}
+
+int sdr_pcd_header(int width, int height, char* buf, size_t cap) {
+    // PCDWriter::generateHeader for PointXYZRGB (rgb written as TYPE U) + writeBinary's DATA line
+    char tmp[512];
+    const int len = std::snprintf(
+        tmp, sizeof(tmp),
+        "# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS x y z rgb\nSIZE 4 4 4 4\n"
+        "TYPE F F F U\nCOUNT 1 1 1 1\nWIDTH %d\nHEIGHT %d\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS %lld\n"
+        "DATA binary\n",
+        width, height, (long long)width * height);
+    if (len < 0) return sdr::set_error(SDR_ERR_ARG, "header formatting failed");
+    if (buf) {
+        if (cap < (size_t)len + 1) return sdr::set_error(SDR_ERR_ARG, "header buffer too small");
+        std::memcpy(buf, tmp, (size_t)len + 1);
+    }
+    return len;
+}
+
+int sdr_write_pcd_binary(const char* path, const void* points, int width, int height) {
+    if (!path || (!points && width * height > 0)) return sdr::set_error(SDR_ERR_ARG, "null argument");
+    if (width < 0 || height < 0) return sdr::set_error(SDR_ERR_ARG, "bad size");
+    char hdr[512];
+    const int len = sdr_pcd_header(width, height, hdr, sizeof(hdr));
+    if (len < 0) return len;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return sdr::set_error(SDR_ERR_ARG, std::string("cannot open ") + path);
+    const size_t nbytes = (size_t)width * height * 16;
+    const bool ok = std::fwrite(hdr, 1, (size_t)len, f) == (size_t)len &&
+                    (nbytes == 0 || std::fwrite(points, 1, nbytes, f) == nbytes);
+    if (std::fclose(f) != 0 || !ok) return sdr::set_error(SDR_ERR_DEVICE, std::string("write failed: ") + path);
+    return SDR_OK;
+}
+
+}  // extern "C"

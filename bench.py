@@ -27,16 +27,31 @@ sys.path.insert(0, ROOT)
 METRIC = "stereo Mpix/s (disparity+reproject) at 1280×720 d=128, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
-# name -> (description, W, H, SGBM args (create order), batch, reproject handleMissing)
+# name -> (description, W, H, SGBM args (create order), batch, reproject handleMissing, kind)
+#   kind "sgbm":  rectified gray pairs -> compute + /16 + reprojectImageTo3D (pcd_write.cpp:111-116)
+#   kind "live":  ZED2 side-by-side BGR -> rectify -> StereoDisparity::computeDisparity (gray,
+#                 INTER_AREA 0.5x, left + right 3WAY, WLS, /16) -> computeDepth
+#                 (stereo_displayer.cpp:155-162, the reference app's per-frame loop)
+#   kind "cloud": side-by-side BGR -> gray -> compute -> reproject(handleMissing) ->
+#                 convertCVMatToPCL(left) -> VoxelGrid(5 mm)   (pcd_write.cpp:81-130)
 CONFIGS = {
     "c2": ("C2 (BASELINE configs[1]): 1280x720 d=128 MODE_SGBM 5-path + reprojectImageTo3D(Q, "
-           "handleMissing), batch 1", 1280, 720, (0, 128, 5, 600, 2400, 1, 63, 12, 200, 2, 0), 1, True),
+           "handleMissing), batch 1", 1280, 720, (0, 128, 5, 600, 2400, 1, 63, 12, 200, 2, 0), 1, True, "sgbm"),
     "c3": ("C3 (configs[2]): 1280x720 d=256 MODE_HH 8-path + reproject, batch 32", 1280, 720,
-           (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, 1), 32, True),
+           (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, 1), 32, True, "sgbm"),
+    "c4": ("C4 (configs[3]): ZED2 2560x720 side-by-side BGR stream -> rectify (config/stereo.yaml maps, "
+           "remap INTER_LINEAR) -> StereoDisparity::computeDisparity (BGR2GRAY, INTER_AREA 0.5x, 3WAY d=80 "
+           "left + right matcher, WLS lambda 8000 sigma 1.1, /16) -> computeDepth; frame shard per GPU + "
+           "RCCL gather of the filtered disparity", 1280, 720, (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1,
+           False, "live"),
+    "c5": ("C5 (configs[4]): 3840x1080 side-by-side BGR (2x1920x1080) -> BGR2GRAY -> MODE_HH 8-path d=256 -> "
+           "reprojectImageTo3D(handleMissing) -> convertCVMatToPCL(left) -> VoxelGrid(5 mm); 8 frames per GPU "
+           "per step (64 across 8 GPUs)", 1920, 1080, (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, 1), 8, True,
+           "cloud"),
     "c0": ("C0 reference-exact matcher: 640x360 d=80 MODE_SGBM_3WAY (stereo_disparity.cpp:5-9) + reproject",
-           640, 360, (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, False),
+           640, 360, (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, False, "sgbm"),
     "pcd": ("pcd_write.cpp:102-116: 1280x720 d=80 MODE_SGBM_3WAY + reproject(handleMissing)", 1280, 720,
-            (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, True),
+            (0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2), 1, True, "sgbm"),
 }
 MODE_NAMES = {0: "MODE_SGBM", 1: "MODE_HH", 2: "MODE_SGBM_3WAY"}
 NPATHS = {0: 5, 1: 8, 2: 3}
@@ -47,23 +62,58 @@ def log(*a):
 
 
 def cpu_baseline(cfg, seconds_target=15.0):
-    """The oracle (C restatement of OpenCV 4.6 SGBM + reprojectImageTo3D) timed on host cores,
-    one frame per thread (ctypes releases the GIL), on a bounded sample."""
+    """The oracle (C restatement of the reference's OpenCV/ximgproc/PCL path) timed on host cores,
+    one frame per thread (ctypes releases the GIL), on a bounded sample of the same workload."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
     from stereo_depth_ruler_amd import synthetic as S
 
-    _, W, H, args, _, hm = cfg
+    _, W, H, args, _, hm, kind = cfg
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
-    L, R, _ = S.make_pair(H, W, args[1], seed=12345)
     p = O.make_params(*args)
+    if kind == "sgbm":
+        L, R, _ = S.make_pair(H, W, args[1], seed=12345)
 
-    def one(_):
-        d = O.sgbm_compute(L, R, p)
-        O.reproject(O.disp_to_float(d), S.REFERENCE_Q, hm)
-        return 1
+        def one(_):
+            d = O.sgbm_compute(L, R, p)
+            O.reproject(O.disp_to_float(d), S.REFERENCE_Q, hm)
+            return 1
+        what = (f"{MODE_NAMES[args[10]]} d={args[1]} full compute (median+speckle) + reproject on {W}x{H} "
+                f"rectified gray pairs")
+    elif kind == "live":
+        from stereo_depth_ruler_amd.config import StereoConfiguration
 
+        cfgf = StereoConfiguration()
+        cfgf.loadFromFile(os.path.join(ROOT, "tests", "golden", "stereo.yaml"))
+        maps = [O.init_undistort_rectify_map(K, Dd, Rr, P, W, H) for K, Dd, Rr, P in (
+            (cfgf.cameraMatrixLeft, cfgf.distCoeffsLeft, cfgf.R1, cfgf.P1),
+            (cfgf.cameraMatrixRight, cfgf.distCoeffsRight, cfgf.R2, cfgf.P2))]
+        frame = S.sbs_bgr_color_frame(H, W, 80, seed=12345)
+        pl = O.make_params(0, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2)
+        pr = O.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2)
+        q = O.wls_params_for_sgbm(0, 80, 5, W // 2, H // 2, 8000.0, 1.1)
+
+        def one(_):
+            gl = O.resize_area_half(O.bgr2gray(O.remap_bilinear(frame[:, :W], *maps[0])))
+            gr = O.resize_area_half(O.bgr2gray(O.remap_bilinear(frame[:, W:], *maps[1])))
+            dl, dr = O.sgbm_compute(gl, gr, pl), O.sgbm_compute(gr, gl, pr)
+            f = O.disp_to_float(O.wls_filter(dl, dr, gl, q))
+            O.reproject(f, cfgf.Q, False)
+            return 1
+        what = ("live-loop frames (remap x2, gray, INTER_AREA, 3WAY d=80 left + right, WLS, /16, reproject) "
+                f"from {2 * W}x{H} side-by-side BGR")
+    else:
+        frame = S.sbs_bgr_color_frame(H, W, args[1], seed=12345)
+
+        def one(_):
+            gl, gr = O.bgr2gray(frame[:, :W]), O.bgr2gray(frame[:, W:])
+            d = O.sgbm_compute(gl, gr, p)
+            xyz = O.reproject(O.disp_to_float(d), S.REFERENCE_Q, hm)
+            O.voxel_grid(O.xyz_to_cloud(xyz, frame[:, :W]), 0.005)
+            return 1
+        what = (f"pcd_write frames (gray, {MODE_NAMES[args[10]]} d={args[1]}, reproject, cloud, VoxelGrid) from "
+                f"{2 * W}x{H} side-by-side BGR")
     frames = 0
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
@@ -75,9 +125,8 @@ def cpu_baseline(cfg, seconds_target=15.0):
         "unit": "Mpix/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{frames} frames of {W}x{H} d={args[1]} {MODE_NAMES[args[10]]} full compute (median+speckle) "
-                  f"+ reproject, {threads} threads x 1 frame each, {el:.1f} s wall; oracle/sgbm_oracle.c "
-                  f"(C restatement of OpenCV 4.6 StereoSGBM; OpenCV itself is absent on this image)",
+        "sample": f"{frames} {what}, {threads} threads x 1 frame each, {el:.1f} s wall; oracle/*.c "
+                  f"(C restatement of OpenCV 4.6 / ximgproc / PCL; those libraries are absent on this image)",
     }
 
 
@@ -126,24 +175,54 @@ def main():
                     "k_wta_lr": _sg.KERNEL_WTA_LR, "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
                     "reproject": _sg.KERNEL_REPROJECT}
 
-    desc, W, H, args, batch, hm = CONFIGS[a.config]
+    desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
     D, mode = args[1], args[10]
     nf = max(a.frames, batch)
-    Ls, Rs = S.make_batch(nf, H, W, D, seed0=1000 * rank)
-    Ld = torch.from_numpy(Ls).to(dev)
-    Rd = torch.from_numpy(Rs).to(dev)
-    # S in-flight frames: one matcher (own scratch) and one HIP stream per slot, frames issued
-    # round-robin, so one frame's compute-bound stages (cost volume, speckle CCL) overlap the
-    # next frame's bandwidth-bound ones (path aggregation, WTA) and the E/W chain tail
     ns = max(1, a.streams)
-    ms = [sdr.StereoSGBM.create(*args, device=dev.index) for _ in range(ns)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
-    disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2 * ns)]
-    xyz = [torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev) for _ in range(ns)]
+    gather_bytes = batch * H * W * 2  # int16 disparity per step
+    if kind == "sgbm":
+        Ls, Rs = S.make_batch(nf, H, W, D, seed0=1000 * rank)
+        Ld = torch.from_numpy(Ls).to(dev)
+        Rd = torch.from_numpy(Rs).to(dev)
+        # S in-flight frames: one matcher (own scratch) and one HIP stream per slot, frames issued
+        # round-robin, so one frame's compute-bound stages (cost volume, speckle CCL) overlap the
+        # next frame's bandwidth-bound ones (path aggregation, WTA) and the E/W chain tail
+        ms = [sdr.StereoSGBM.create(*args, device=dev.index) for _ in range(ns)]
+        disp = [torch.empty((batch, H, W), dtype=torch.int16, device=dev) for _ in range(2 * ns)]
+        xyz = [torch.empty((batch, H, W, 3), dtype=torch.float32, device=dev) for _ in range(ns)]
+        closers = ms
+
+        def run(j, k, slot):
+            ms[k].compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot],
+                                    xyz=xyz[k])
+            return disp[slot]
+    else:
+        from stereo_depth_ruler_amd.config import StereoConfiguration
+        from stereo_depth_ruler_amd.pipeline import CloudEmit, LiveLoop
+        from stereo_depth_ruler_amd.rectify import StereoRectifier
+
+        sbs = torch.empty((nf, H, 2 * W, 3), dtype=torch.uint8, device=dev)
+        for i in range(nf):
+            sbs[i].copy_(torch.from_numpy(S.sbs_bgr_color_frame(H, W, D if kind == "cloud" else 80,
+                                                                seed=1000 * rank + i)))
+        if kind == "live":
+            cfg = StereoConfiguration()
+            assert cfg.loadFromFile(os.path.join(ROOT, "tests", "golden", "stereo.yaml"))
+            rect = StereoRectifier(cfg, device=dev.index)
+            pipes = [LiveLoop(rect, cfg.Q, batch, device=dev.index, args=args) for _ in range(ns)]
+            gather_bytes = batch * (H // 2) * (W // 2) * 2
+        else:
+            pipes = [CloudEmit(W, H, args, batch, S.REFERENCE_Q, device=dev.index) for _ in range(ns)]
+        ms = [p.matcher() for p in pipes]
+        closers = pipes
+
+        def run(j, k, slot):
+            return pipes[k].enqueue(sbs[j:j + batch], streams[k])
     m = ms[0]
     gather_bufs = None
     if world > 1 and rank == 0:  # RCCL has no int16: gather the disparity bytes
-        gather_bufs = [[torch.empty(batch * H * W * 2, dtype=torch.uint8, device=dev) for _ in range(world)]
+        gather_bufs = [[torch.empty(gather_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
                        for _ in range(2 * ns)]
     pending = [None] * (2 * ns)
 
@@ -155,11 +234,14 @@ def main():
             pending[slot].wait()
             pending[slot] = None
         with torch.cuda.stream(streams[k]):
-            ms[k].compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[slot],
-                                    xyz=xyz[k])
+            res = run(j, k, slot)
             if world > 1:
-                pending[slot] = dist.gather(as_bytes(disp[slot]), gather_bufs[slot] if rank == 0 else None,
-                                            dst=0, async_op=True)
+                # gather this step's disparity from every rank; a later step reuses the slot only
+                # after this collective has completed
+                src = as_bytes(res) if res.dtype != torch.uint8 else res
+                pending[slot] = dist.gather(src.reshape(-1).clone() if kind != "sgbm" else src,
+                                            gather_bufs[slot] if rank == 0 else None, dst=0,
+                                            async_op=True)
 
     for i in range(a.warmup):
         step(i)
@@ -190,8 +272,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    w1 = W - max(args[0] + D, 0) + min(args[0], 0)
-    cells = batch * H * w1 * D
+    Wm, Hm = (W // 2, H // 2) if kind == "live" else (W, H)  # the left matcher's frame
+    w1 = Wm - max(args[0] + D, 0) + min(args[0], 0)
+    cells = batch * Hm * w1 * D
     P = NPATHS[mode]
 
     def kernel_report(mm):
@@ -248,9 +331,10 @@ def main():
             # timed region (kernel quality; the timed region's numbers include the overlap)
             torch.cuda.synchronize()
             m.kernel_time(-1, reset=True)
-            for i in range(a.iso_steps):
-                j = (i * batch) % (nf - batch + 1) if nf > batch else 0
-                m.compute_reproject(Ld[j:j + batch], Rd[j:j + batch], S.REFERENCE_Q, hm, disp=disp[0], xyz=xyz[0])
+            with torch.cuda.stream(streams[0]):
+                for i in range(a.iso_steps):
+                    j = (i * batch) % (nf - batch + 1) if nf > batch else 0
+                    run(j, 0, 0)
             torch.cuda.synchronize()
             iso_k, iso_r = kernel_report(m)
             iso_r["measured"] = f"HIP events, {a.iso_steps} single-stream steps after the timed region"
@@ -272,11 +356,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int16",
-        "data": "synthetic seeded rectified pairs (SURVEY.md 8d recipe); reference assets absent",
+        "data": ("synthetic seeded rectified pairs (SURVEY.md 8d recipe); reference assets absent" if kind == "sgbm"
+                 else "synthetic seeded side-by-side BGR frames (SURVEY.md 8d recipe); reference assets absent"),
         "config": {
             "workload": desc,
             "width": W, "height": H, "numDisparities": D, "mode": MODE_NAMES[mode],
-            "paths": NPATHS[mode], "batch": batch,
+            "paths": NPATHS[mode], "batch": batch, "pipeline": kind,
             "params": dict(zip(["minDisparity", "numDisparities", "blockSize", "P1", "P2",
                                 "disp12MaxDiff", "preFilterCap", "uniquenessRatio",
                                 "speckleWindowSize", "speckleRange", "mode"], args)),
@@ -295,7 +380,7 @@ def main():
             log("cpu baseline failed:", repr(e))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for mm in ms:
+    for mm in closers:
         mm.close()
     if world > 1:
         dist.barrier()

@@ -245,10 +245,12 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
 /* ---- point-cloud emit after the path, point_cloud/src/pcd_write.cpp ----
  * Points are pcl::PointXYZRGB as savePCDFileBinary lays them out: 16-byte records
  * {float x, y, z; uint32 rgba}. */
-/* convertCVMatToPCL(xyz, left) (pcd_write.cpp:17-51): xyz float [F][H][W][3], bgr u8 [F][H][W][3]
- * or NULL -> organised cloud [F][H*W]; non-finite points get NaN x/y/z. Async on `stream`. */
-int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, int width, int height,
-                            int nframes, void* d_points, void* stream);
+/* convertCVMatToPCL(xyz, left) (pcd_write.cpp:17-51): xyz float [F][H][W][3], bgr u8 3-channel
+ * rows of bgr_stride bytes, frames bgr_frame_stride apart (0 = dense), or NULL -> organised cloud
+ * [F][H*W]; non-finite points get NaN x/y/z.  Async on `stream`. */
+int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, size_t bgr_stride,
+                            size_t bgr_frame_stride, int width, int height, int nframes,
+                            void* d_points, void* stream);
 /* pcl::VoxelGrid<PointXYZRGB> with leaf (lx, ly, lz) (pcd_write.cpp:122-130) on n device points
  * -> d_out (capacity n) and *out_count.  PCL's int32-overflow case (leaf too small for the extent,
  * the reference's 5 mm leaf on millimetre clouds) copies the input through and sets *passthrough.

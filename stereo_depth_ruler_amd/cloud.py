@@ -46,8 +46,8 @@ def convertCVMatToPCL(xyz, bgr=None) -> PointCloud:
         if tuple(b.shape) != (h, w, 3):
             b = None  # hasColor: colour only when the image has the cloud's size
     out = torch.empty((h * w, 4), dtype=torch.float32, device=dev)
-    check(lib().sdr_xyz_to_cloud_device(x.data_ptr(), None if b is None else b.data_ptr(), w, h, 1,
-                                        out.data_ptr(), _cstream(dev.index)))
+    check(lib().sdr_xyz_to_cloud_device(x.data_ptr(), None if b is None else b.data_ptr(), 0, 0, w, h,
+                                        1, out.data_ptr(), _cstream(dev.index)))
     if host:
         torch.cuda.synchronize(dev)
         out = out.cpu().numpy()

@@ -31,7 +31,8 @@ __device__ __forceinline__ bool finite3(float x, float y, float z) {
 }
 
 __global__ __launch_bounds__(256) void k_xyz_to_cloud(const float* __restrict__ xyz,
-                                                      const uint8_t* __restrict__ bgr, size_t n,
+                                                      const uint8_t* __restrict__ bgr, int W, int H,
+                                                      size_t bstride, size_t bfstride, size_t n,
                                                       float4* __restrict__ out) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         const float x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
@@ -41,7 +42,11 @@ __global__ __launch_bounds__(256) void k_xyz_to_cloud(const float* __restrict__ 
             o.x = x;
             o.y = y;
             o.z = z;
-            if (bgr) rgba |= (uint32_t)bgr[3 * i + 2] << 16 | (uint32_t)bgr[3 * i + 1] << 8 | bgr[3 * i];
+            if (bgr) {
+                const size_t f = i / ((size_t)W * H), r = i % ((size_t)W * H);
+                const uint8_t* px = bgr + f * bfstride + (r / W) * bstride + (r % W) * 3;
+                rgba |= (uint32_t)px[2] << 16 | (uint32_t)px[1] << 8 | px[0];
+            }
         } else {
             o.x = o.y = o.z = __uint_as_float(0x7FC00000u);
         }
@@ -176,14 +181,18 @@ struct AsyncScratch {
 
 extern "C" {
 
-int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, int width, int height,
-                            int nframes, void* d_points, void* stream) {
+int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, size_t bgr_stride,
+                            size_t bgr_frame_stride, int width, int height, int nframes,
+                            void* d_points, void* stream) {
     if (!d_xyz || !d_points) return sdr::set_error(SDR_ERR_ARG, "null argument");
     if (width <= 0 || height <= 0 || nframes <= 0) return sdr::set_error(SDR_ERR_ARG, "bad size");
+    if (!bgr_stride) bgr_stride = (size_t)width * 3;
+    if (!bgr_frame_stride) bgr_frame_stride = bgr_stride * height;
+    if (d_bgr && bgr_stride < (size_t)width * 3) return sdr::set_error(SDR_ERR_ARG, "bad BGR stride");
     const size_t n = (size_t)width * height * nframes;
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
     hipLaunchKernelGGL(sdr::k_xyz_to_cloud, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_xyz,
-                       d_bgr, n, (float4*)d_points);
+                       d_bgr, width, height, bgr_stride, bgr_frame_stride, n, (float4*)d_points);
     CLOUD_HIP(hipGetLastError());
     return SDR_OK;
 }

@@ -13,11 +13,12 @@
 //   k_wls_conf     left discontinuity (inline) + discontinuity-aware LR check -> confidence
 //                  x255 (full map for getConfidenceMap) and the two FGS inputs conf*d, conf,
 //                  compacted to the ROI
-//   k_fgs_lines    one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
+//   k_fgs_sweep    one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
 //                  BOTH inputs at once (the elimination coefficients depend only on the guide
-//                  and lambda).  A wave owns 64 lines; the lines are walked in 64-element chunks
-//                  staged through LDS with coalesced loads (rows and columns alike), so the
-//                  serial per-line recurrence reads LDS, never HBM
+//                  and lambda).  Lane = line over k-major data (coalesced), loads PF samples
+//                  ahead in registers, so a step costs the t-recurrence's division latency
+//   k_transpose2   LDS-tiled transposes between the row pass's column-major copies and the
+//                  column pass's row-major images; k_fgs_weights builds both weight layouts once
 //   k_wls_final    FGS(conf*d) / FGS(conf) -> saturate_cast<short>, 16*(min_disp-1) outside ROI
 #include "../../include/sdr/sdr.h"
 #include "sdr_internal.hpp"
@@ -128,148 +129,159 @@ __global__ __launch_bounds__(256) void k_wls_conf(const int16_t* __restrict__ dl
 //   k>0:  a = lam*C[k-1];  c = lam*C[k];  den = (1 - c) - a*(1 + t[k-1]);
 //         t[k] = c / den;  u_k = (u_k - a*u_{k-1}) / den
 //   back: u_k = u_k - t[k]*u_{k+1}
-// ROWS: line l = row l (element k at l*pitch + k); else line l = column l (element at k*pitch + l).
-constexpr int kChunk = 64;
-constexpr int kTilePitch = kChunk + 1;  // conflict-free row reads of the [line][k] tile
+//
+// Layout: a sweep runs over "k-major" arrays, element (line l, sample k) at k*nlines + l, so that
+// the 64 lanes of a wave (64 consecutive lines) touch 256 contiguous bytes per sample.  The row
+// pass therefore works on column-major copies and the column pass on row-major ones; k_transpose2
+// moves both right-hand sides between the two (LDS tiles).  Each lane walks its line with the
+// loads of the next PF samples in flight (register ring), so a step costs the dependent-division
+// latency of the t recurrence, not a memory round trip.
+constexpr int kFgsPF = 8;
 
-template <bool ROWS>
-__global__ __launch_bounds__(64) void k_fgs_lines(const uint8_t* __restrict__ guide,
-                                                  size_t gstride, size_t gfstride,
-                                                  const float* __restrict__ lut, float* U0,
-                                                  float* U1, float* T, int nimg, int w, int h,
-                                                  float lam) {
-    __shared__ float sU0[kChunk * kTilePitch];
-    __shared__ float sU1[kChunk * kTilePitch];
-    // the weights C[k] and the coefficients t[k] share a tile: iteration k reads C[k], then
-    // writes t[k] over it
-    __shared__ float sT[kChunk * kTilePitch];
-    float* sC = sT;
-    const int lane = threadIdx.x;
-    const int nlines = ROWS ? h : w;
-    const int n = ROWS ? w : h;
-    const int l0 = blockIdx.x * kChunk;
-    const int f = blockIdx.y;
-    const uint8_t* gf = guide + (size_t)f * gfstride;
-    const size_t fo = (size_t)f * w * h;
-    float* u0 = U0 + fo;
-    float* u1 = nimg > 1 ? U1 + fo : nullptr;
-    float* t = T + fo;
-    const int nl = min(kChunk, nlines - l0);
-    auto eidx = [&](int l, int k) -> size_t {
-        return ROWS ? (size_t)l * w + k : (size_t)k * w + l;
-    };
-    auto gval = [&](int l, int k) -> int {
-        return ROWS ? gf[(size_t)l * gstride + k] : gf[(size_t)k * gstride + l];
-    };
-    const bool active = lane < nl;
-    // forward elimination, chunk by chunk
-    float cprev = 0.0f, tprev = 0.0f, p0 = 0.0f, p1 = 0.0f;
-    for (int k0 = 0; k0 < n; k0 += kChunk) {
-        const int nk = min(kChunk, n - k0);
-        // stage U (and C) tiles [line][k]: each pass loads 64 consecutive addresses
-        for (int r = 0; r < kChunk; r++) {
-            int l, k;
-            if (ROWS) { l = r; k = lane; } else { l = lane; k = r; }
-            if (l < nl && k < nk) {
-                const int gl = l0 + l, gk = k0 + k;
-                const size_t e = eidx(gl, gk);
-                sU0[l * kTilePitch + k] = u0[e];
-                if (u1) sU1[l * kTilePitch + k] = u1[e];
-                float cw = 0.0f;
-                if (gk + 1 < n) {
-                    const int dv = gval(gl, gk) - gval(gl, gk + 1);
-                    cw = lut[dv * dv];
-                }
-                sC[l * kTilePitch + k] = cw;
-            }
-        }
-        __syncthreads();
-        if (active) {
-            float* r0 = sU0 + lane * kTilePitch;
-            float* r1 = sU1 + lane * kTilePitch;
-            float* rt = sT + lane * kTilePitch;
-            const float* rc = sC + lane * kTilePitch;
-            int k = 0;
-            if (k0 == 0) {
-                cprev = rc[0];
-                const float c0 = lam * cprev;
-                const float den = 1.0f - c0;
-                tprev = c0 / den;
-                rt[0] = tprev;
-                p0 = r0[0] / den;
-                r0[0] = p0;
-                if (u1) { p1 = r1[0] / den; r1[0] = p1; }
-                k = 1;
-            }
-            for (; k < nk; k++) {
-                const float a = lam * cprev;
-                const float ck = rc[k];
-                const float c = lam * ck;
-                const float den = (1.0f - c) - a * (1.0f + tprev);
-                tprev = c / den;
-                rt[k] = tprev;
-                p0 = (r0[k] - a * p0) / den;
-                r0[k] = p0;
-                if (u1) { p1 = (r1[k] - a * p1) / den; r1[k] = p1; }
-                cprev = ck;
-            }
-        }
-        __syncthreads();
-        for (int r = 0; r < kChunk; r++) {
-            int l, k;
-            if (ROWS) { l = r; k = lane; } else { l = lane; k = r; }
-            if (l < nl && k < nk) {
-                const size_t e = eidx(l0 + l, k0 + k);
-                u0[e] = sU0[l * kTilePitch + k];
-                if (u1) u1[e] = sU1[l * kTilePitch + k];
-                t[e] = sT[l * kTilePitch + k];
-            }
-        }
-        __syncthreads();
+__global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1, const float* __restrict__ Cw,
+                                                  float* __restrict__ T, int nlines, int n,
+                                                  size_t fstride, float lam) {
+    constexpr int PF = kFgsPF;
+    const int l = blockIdx.x * 64 + threadIdx.x;
+    if (l >= nlines) return;
+    const size_t base = (size_t)blockIdx.y * fstride + l;
+    float* u0 = U0 + base;
+    float* u1 = U1 ? U1 + base : nullptr;
+    const float* cw = Cw + base;
+    float* t = T + base;
+    const size_t st = (size_t)nlines;
+    const int last = n - 1;
+    // ---- forward elimination ----
+    float r0[PF], r1[PF], rc[PF];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const size_t o = (size_t)min(j, last) * st;
+        r0[j] = u0[o];
+        r1[j] = u1 ? u1[o] : 0.0f;
+        rc[j] = cw[o];
     }
-    // back substitution, chunks in reverse (the last chunk is re-read from L2)
-    float q0 = 0.0f, q1 = 0.0f;
-    const int last0 = ((n - 1) / kChunk) * kChunk;
-    for (int k0 = last0; k0 >= 0; k0 -= kChunk) {
-        const int nk = min(kChunk, n - k0);
-        for (int r = 0; r < kChunk; r++) {
-            int l, k;
-            if (ROWS) { l = r; k = lane; } else { l = lane; k = r; }
-            if (l < nl && k < nk) {
-                const size_t e = eidx(l0 + l, k0 + k);
-                sU0[l * kTilePitch + k] = u0[e];
-                if (u1) sU1[l * kTilePitch + k] = u1[e];
-                sT[l * kTilePitch + k] = t[e];
+    float cprev = 0.0f, tprev = 0.0f, p0 = 0.0f, p1 = 0.0f;
+    for (int k0 = 0; k0 < n; k0 += PF) {
+        float n0[PF], n1[PF], nc[PF];
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const size_t o = (size_t)min(k0 + PF + j, last) * st;
+            n0[j] = u0[o];
+            n1[j] = u1 ? u1[o] : 0.0f;
+            nc[j] = cw[o];
+        }
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const int k = k0 + j;
+            if (k <= last) {
+                const size_t o = (size_t)k * st;
+                if (k == 0) {
+                    const float c0 = lam * rc[j];
+                    const float den = 1.0f - c0;
+                    tprev = c0 / den;
+                    p0 = r0[j] / den;
+                    if (u1) p1 = r1[j] / den;
+                } else {
+                    const float aa = lam * cprev;
+                    const float c = lam * rc[j];
+                    const float den = (1.0f - c) - aa * (1.0f + tprev);
+                    tprev = c / den;
+                    p0 = (r0[j] - aa * p0) / den;
+                    if (u1) p1 = (r1[j] - aa * p1) / den;
+                }
+                cprev = rc[j];
+                t[o] = tprev;
+                u0[o] = p0;
+                if (u1) u1[o] = p1;
             }
         }
-        __syncthreads();
-        if (active) {
-            float* r0 = sU0 + lane * kTilePitch;
-            float* r1 = sU1 + lane * kTilePitch;
-            const float* rt = sT + lane * kTilePitch;
-            int k = nk - 1;
-            if (k0 + k == n - 1) {  // the last sample keeps its forward value
-                q0 = r0[k];
-                if (u1) q1 = r1[k];
-                k--;
-            }
-            for (; k >= 0; k--) {
-                q0 = r0[k] - rt[k] * q0;
-                r0[k] = q0;
-                if (u1) { q1 = r1[k] - rt[k] * q1; r1[k] = q1; }
+#pragma unroll
+        for (int j = 0; j < PF; j++) { r0[j] = n0[j]; r1[j] = n1[j]; rc[j] = nc[j]; }
+    }
+    // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
+    float q0 = p0, q1 = p1;
+    float b0[PF], b1[PF], bt[PF];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const size_t o = (size_t)max(last - 1 - j, 0) * st;
+        b0[j] = u0[o];
+        b1[j] = u1 ? u1[o] : 0.0f;
+        bt[j] = t[o];
+    }
+    for (int k0 = last - 1; k0 >= 0; k0 -= PF) {
+        float n0[PF], n1[PF], nt[PF];
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const size_t o = (size_t)max(k0 - PF - j, 0) * st;
+            n0[j] = u0[o];
+            n1[j] = u1 ? u1[o] : 0.0f;
+            nt[j] = t[o];
+        }
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const int k = k0 - j;
+            if (k >= 0) {
+                const size_t o = (size_t)k * st;
+                q0 = b0[j] - bt[j] * q0;
+                u0[o] = q0;
+                if (u1) {
+                    q1 = b1[j] - bt[j] * q1;
+                    u1[o] = q1;
+                }
             }
         }
-        __syncthreads();
-        for (int r = 0; r < kChunk; r++) {
-            int l, k;
-            if (ROWS) { l = r; k = lane; } else { l = lane; k = r; }
-            if (l < nl && k < nk) {
-                const size_t e = eidx(l0 + l, k0 + k);
-                u0[e] = sU0[l * kTilePitch + k];
-                if (u1) u1[e] = sU1[l * kTilePitch + k];
-            }
+#pragma unroll
+        for (int j = 0; j < PF; j++) { b0[j] = n0[j]; b1[j] = n1[j]; bt[j] = nt[j]; }
+    }
+}
+
+// FGS weights of one guide (per frame): ChT (column-major, for the row pass: weight between
+// (i, j) and (i, j+1) at j*h + i) and Cv (row-major, for the column pass: (i, j)-(i+1, j) at i*w + j)
+__global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__ guide, size_t gstride,
+                                                     size_t gfstride, const float* __restrict__ lut,
+                                                     int w, int h, float* __restrict__ ChT,
+                                                     float* __restrict__ Cv) {
+    const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (j >= w || i >= h) return;
+    const uint8_t* g = guide + (size_t)blockIdx.z * gfstride + (size_t)i * gstride + j;
+    const size_t fo = (size_t)blockIdx.z * w * h;
+    const int v = g[0];
+    float ch = 0.0f, cv = 0.0f;
+    if (j + 1 < w) {
+        const int d = v - g[1];
+        ch = lut[d * d];
+    }
+    if (i + 1 < h) {
+        const int d = v - g[gstride];
+        cv = lut[d * d];
+    }
+    ChT[fo + (size_t)j * h + i] = ch;
+    Cv[fo + (size_t)i * w + j] = cv;
+}
+
+// dst[f][c][r] = src[f][r][c] for two arrays (rows x cols per frame), 64x64 LDS tiles
+__global__ __launch_bounds__(256) void k_transpose2(const float* __restrict__ s0,
+                                                    const float* __restrict__ s1, float* __restrict__ d0,
+                                                    float* __restrict__ d1, int rows, int cols) {
+    __shared__ float tile[2][64][65];
+    const int c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+    const size_t fo = (size_t)blockIdx.z * rows * cols;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int rr = r0 + r, cc = c0 + tx;
+        if (rr < rows && cc < cols) {
+            tile[0][r][tx] = s0[fo + (size_t)rr * cols + cc];
+            if (s1) tile[1][r][tx] = s1[fo + (size_t)rr * cols + cc];
         }
-        __syncthreads();
+    }
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {
+        const int cc = c0 + c, rr = r0 + tx;
+        if (rr < rows && cc < cols) {
+            d0[fo + (size_t)cc * rows + rr] = tile[0][tx][c];
+            if (s1) d1[fo + (size_t)cc * rows + rr] = tile[1][tx][c];
+        }
     }
 }
 
@@ -296,16 +308,31 @@ __global__ __launch_bounds__(256) void k_wls_final(const float* __restrict__ A,
     out[o] = r;
 }
 
+// FastGlobalSmootherFilter::filter on nimg (1 or 2) row-major w x h images per frame (R0, R1, in
+// place), F frames sharing per-frame guides.  Scratch (each F*w*h floats): A, B (column-major
+// copies), T (elimination coefficients), ChT, Cv (weights).
+struct FgsScratch {
+    float *A, *B, *T, *ChT, *Cv;
+};
+
 static void launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
-                       float* U0, float* U1, float* T, int nimg, int w, int h, int F,
-                       double lambda, double att, int iters, hipStream_t st) {
+                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
+                       int iters, const FgsScratch& s, hipStream_t st) {
+    const size_t fs = (size_t)w * h;
+    hipLaunchKernelGGL(k_fgs_weights, dim3((w + 63) / 64, (h + 3) / 4, F), dim3(256), 0, st, guide,
+                       gstride, gfstride, lut, w, h, s.ChT, s.Cv);
+    const dim3 t_rm((w + 63) / 64, (h + 63) / 64, F), t_cm((h + 63) / 64, (w + 63) / 64, F);
     float lam = (float)lambda;
     const float fa = (float)att;
     for (int it = 0; it < iters; it++) {
-        hipLaunchKernelGGL(k_fgs_lines<true>, dim3((h + kChunk - 1) / kChunk, F), dim3(64), 0, st,
-                           guide, gstride, gfstride, lut, U0, U1, T, nimg, w, h, lam);
-        hipLaunchKernelGGL(k_fgs_lines<false>, dim3((w + kChunk - 1) / kChunk, F), dim3(64), 0, st,
-                           guide, gstride, gfstride, lut, U0, U1, T, nimg, w, h, lam);
+        // row pass on column-major copies (lines = rows, k = column)
+        hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
+        hipLaunchKernelGGL(k_fgs_sweep, dim3((h + 63) / 64, F), dim3(64), 0, st, s.A,
+                           R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
+        hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
+        // column pass in place on the row-major images (lines = columns, k = row)
+        hipLaunchKernelGGL(k_fgs_sweep, dim3((w + 63) / 64, F), dim3(64), 0, st, R0, R1, s.Cv, s.T, w,
+                           h, fs, lam);
         lam = lam * fa;  // FastGlobalSmootherFilterImpl::filter: lambda *= lambda_attenuation
     }
 }
@@ -327,7 +354,7 @@ struct sdr_wls {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    sdr::Buf rdisc, conf, A, B, T, lut, out, hbuf;
+    sdr::Buf rdisc, conf, A, B, Ac, Bc, T, ChT, Cv, lut, out, hbuf;
     double lut_sigma = -1.0;
 };
 
@@ -410,7 +437,8 @@ int sdr_wls_destroy(sdr_wls* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (sdr::Buf* b : {&h->rdisc, &h->conf, &h->A, &h->B, &h->T, &h->lut, &h->out, &h->hbuf})
+    for (sdr::Buf* b : {&h->rdisc, &h->conf, &h->A, &h->B, &h->Ac, &h->Bc, &h->T, &h->ChT, &h->Cv,
+                        &h->lut, &h->out, &h->hbuf})
         if (b->p) (void)hipFree(b->p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -483,9 +511,8 @@ int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, cons
     int rc;
     const float* lut = nullptr;
     if ((rc = sdr::ensure(h->rdisc, F * px * 4))) return rc;
-    if ((rc = sdr::ensure(h->A, F * cpx * 4 + 4))) return rc;
-    if ((rc = sdr::ensure(h->B, F * cpx * 4 + 4))) return rc;
-    if ((rc = sdr::ensure(h->T, F * cpx * 4 + 4))) return rc;
+    for (sdr::Buf* b : {&h->A, &h->B, &h->Ac, &h->Bc, &h->T, &h->ChT, &h->Cv})
+        if ((rc = sdr::ensure(*b, F * cpx * 4 + 4))) return rc;
     if ((rc = upload_lut(h, p.sigma_color, &lut))) return rc;
     float* A = (float*)h->A.p;
     float* B = (float*)h->B.p;
@@ -499,8 +526,10 @@ int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, cons
                        conf, A, B);
     if (roi) {
         const uint8_t* g0 = guide + (size_t)g.ry * gstride + g.rx;
-        sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, (float*)h->T.p, 2, g.rw, g.rh, F,
-                        p.lambda, p.lambda_attenuation, p.num_iter, st);
+        const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
+                                 (float*)h->Cv.p};
+        sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
+                        p.lambda_attenuation, p.num_iter, fs, st);
     }
     hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out);
     WLS_HIP(hipGetLastError());
@@ -545,22 +574,23 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
     hipStream_t st = (hipStream_t)stream;
     std::vector<float> lut;
     sdr::fgs_lut_host(sigma, &lut);
-    // stream-ordered scratch: LUT + elimination coefficients
+    // stream-ordered scratch: LUT, column-major copies, coefficients, weights
     float* dlut = nullptr;
-    float* T = nullptr;
+    float* scr = nullptr;
     const size_t px = (size_t)w * h;
     WLS_HIP(hipMallocAsync((void**)&dlut, sizeof(float) * lut.size(), st));
-    WLS_HIP(hipMallocAsync((void**)&T, sizeof(float) * px * 2, st));
+    WLS_HIP(hipMallocAsync((void**)&scr, sizeof(float) * px * 5, st));
     WLS_HIP(hipMemcpyAsync(dlut, lut.data(), sizeof(float) * lut.size(), hipMemcpyHostToDevice, st));
+    const sdr::FgsScratch fs{scr, scr + px, scr + 2 * px, scr + 3 * px, scr + 4 * px};
     // images are filtered in pairs (two right-hand sides of one system per line)
     for (int i = 0; i < nimg; i += 2) {
         const int m = nimg - i >= 2 ? 2 : 1;
         sdr::launch_fgs(d_guide, gstride, 0, dlut, d_img + i * px, m == 2 ? d_img + (i + 1) * px : nullptr,
-                        T, m, w, h, 1, lambda, att, iters, st);
+                        w, h, 1, lambda, att, iters, fs, st);
     }
     WLS_HIP(hipGetLastError());
     WLS_HIP(hipFreeAsync(dlut, st));
-    WLS_HIP(hipFreeAsync(T, st));
+    WLS_HIP(hipFreeAsync(scr, st));
     // the host LUT vector dies here: wait for its upload before returning
     WLS_HIP(hipStreamSynchronize(st));
     return SDR_OK;

@@ -96,3 +96,16 @@ def sbs_bgr_frame(h: int, w: int, num_disp: int, seed: int = 0):
     frame[:, :w, :] = left[:, :, None]
     frame[:, w:, :] = right[:, :, None]
     return frame
+
+
+def sbs_bgr_color_frame(h: int, w: int, num_disp: int, seed: int = 0):
+    """A ZED2-style side-by-side BGR frame (h x 2w x 3) whose channels differ: B = the seeded gray
+    view, G = the view shifted by one column, R = seeded noise (so BGR2GRAY is exercised)."""
+    left, right, _ = make_pair(h, w, num_disp, seed)
+    rng = np.random.default_rng(seed + 7)
+    frame = np.empty((h, 2 * w, 3), np.uint8)
+    for k, v in enumerate((left, right)):
+        frame[:, k * w:(k + 1) * w, 0] = v
+        frame[:, k * w:(k + 1) * w, 1] = np.roll(v, 1, 1)
+        frame[:, k * w:(k + 1) * w, 2] = rng.integers(0, 256, v.shape, dtype=np.uint8)
+    return frame

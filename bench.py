@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="frames in flight (one matcher + stream each)")
+    ap.add_argument("--streams", type=int, default=3, help="frames in flight (one matcher + stream each)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
     a = ap.parse_args()
 

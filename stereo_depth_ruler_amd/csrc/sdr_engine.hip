@@ -133,7 +133,7 @@ struct sdr_sgbm {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz;
+    Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz, keys2;
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -182,17 +182,18 @@ static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
         aux = (size_t)st->size() * amax * std::max(g.W1, 0) * g.D * 2;
     }
     const size_t px = (size_t)g.W * g.H;
-    return (size_t)F * (6 * px * 8 + cells * 2 * (1 + npaths_of(e.mode)) + aux + px * 2 * 3 +
+    return (size_t)F * (6 * px * 8 + cells * 2 * npaths_of(e.mode) + aux + px * 2 * 3 + px * 4 +
                         px * 4 * 2);
 }
 
 static int npaths_of(int mode) { return mode == SDR_MODE_HH ? 8 : mode == SDR_MODE_SGBM ? 5 : 3; }
 
 // Enqueues the full compute for F frames whose inputs are already on the device.
-//   prefilter -> cost volume (+ 3WAY stripe-start rows) -> all path directions in one launch,
-//   each into its own L buffer -> WTA/uniqueness/subpixel/disp2/LR per row -> median3 -> speckle
-// Per cell this moves 2 (C write) + 4P (paths: C read + L write) + 2P (WTA: L reads) bytes,
-// the canonical 2 + 6P of SURVEY.md 8(d).
+//   prefilter -> cost volume (+ 3WAY stripe-start rows) -> the P-1 directions other than
+//   top-to-bottom in one launch, each into its own L buffer -> top-to-bottom chains fused with
+//   WTA/uniqueness/subpixel/disp2 -> LR check -> median3 -> speckle
+// Per cell this moves 2 (C write) + 4(P-1) (paths: C read + L write) + 2 + 2(P-1) (fused pass:
+// C read + the other L reads) = 6P - 2 bytes, 4 fewer than the canonical 2 + 6P of SURVEY.md 8(d).
 //   out (nullable): dense [F][H][W] int16 destination for the final map (else internal buffer)
 //   out_min (nullable): per-frame minimum of the final map (reprojectImageTo3D handleMissing)
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
@@ -228,8 +229,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
 
     if ((rc = ensure(h->planesL, F * 3 * px * 8))) return rc;
     if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
-    if ((rc = ensure(h->C, F * cells * 2))) return rc;
-    if ((rc = ensure(h->Lr, (size_t)P * F * cells * 2))) return rc;
+    const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;  // k_south_wta's load overrun
+    if ((rc = ensure(h->C, (F * cells + slack) * 2))) return rc;
+    if ((rc = ensure(h->Lr, ((size_t)(P - 1) * F * cells + slack) * 2))) return rc;
+    if ((rc = ensure(h->keys2, F * px * 4))) return rc;
     if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
     if ((rc = ensure(h->draw, F * px * 2))) return rc;
     if ((rc = ensure(h->dlr, F * px * 2))) return rc;
@@ -281,13 +284,15 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));
 
-    sdr::PathLaunch pls{};
-    pls.C = C;
-    pls.cs_fstride = cells;
-    pls.aux_fstride = aux_fstride;
-    pls.ndirs = 0;
+    // k_paths: every direction except the top-to-bottom one, each into its own L buffer (in the
+    // order E, W, [S], SE, SW, N, NE, NW that k_wta_lr's sum uses); k_south_wta: the
+    // top-to-bottom chains fused with the WTA, reading the other P-1 buffers
+    sdr::PathLaunch pls{}, plS{};
+    pls.C = plS.C = C;
+    pls.cs_fstride = plS.cs_fstride = cells;
+    pls.aux_fstride = plS.aux_fstride = aux_fstride;
     int nbuf = 0;
-    auto add_dir = [&](int dir, int nch, int16_t* out) {
+    auto add_dir = [&](sdr::PathLaunch& pl, int dir, int nch, int16_t* out) {
         sdr::PathDir d{};
         d.dir = dir;
         d.nchains = nch;
@@ -295,19 +300,18 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         d.yend = H;
         d.write_from = 0;
         d.out = out;
-        pls.d[pls.ndirs++] = d;
+        pl.d[pl.ndirs++] = d;
     };
     auto buf = [&]() { return Lr + (size_t)(nbuf++) * F * cells; };
     const int nE = H, nS = g.W1, nD = g.W1 + H - 1;
     // longest chains first: the E/W rows (W1 steps) are dispatched before the shorter ones
-    add_dir(sdr::DIR_E, nE, buf());
-    add_dir(sdr::DIR_W, nE, buf());
+    add_dir(pls, sdr::DIR_E, nE, buf());
+    add_dir(pls, sdr::DIR_W, nE, buf());
     if (e.mode == SDR_MODE_SGBM_3WAY) {
-        int16_t* out = buf();
         for (size_t s = 0; s < stripes.size(); s++) {
             const Stripe& sp = stripes[s];
-            add_dir(sdr::DIR_S, nS, out);
-            sdr::PathDir& d = pls.d[pls.ndirs - 1];
+            add_dir(plS, sdr::DIR_S, nS, nullptr);
+            sdr::PathDir& d = plS.d[plS.ndirs - 1];
             d.ybeg = sp.s0;
             d.yend = sp.end;
             d.write_from = sp.out0;
@@ -318,31 +322,32 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             }
         }
     } else {
-        add_dir(sdr::DIR_S, nS, buf());
-        if (e.mode == SDR_MODE_HH) add_dir(sdr::DIR_N, nS, buf());
-        add_dir(sdr::DIR_SE, nD, buf());
-        add_dir(sdr::DIR_SW, nD, buf());
+        add_dir(plS, sdr::DIR_S, nS, nullptr);
+        if (e.mode == SDR_MODE_HH) add_dir(pls, sdr::DIR_N, nS, buf());
+        add_dir(pls, sdr::DIR_SE, nD, buf());
+        add_dir(pls, sdr::DIR_SW, nD, buf());
         if (e.mode == SDR_MODE_HH) {
-            add_dir(sdr::DIR_NE, nD, buf());
-            add_dir(sdr::DIR_NW, nD, buf());
+            add_dir(pls, sdr::DIR_NE, nD, buf());
+            add_dir(pls, sdr::DIR_NW, nD, buf());
         }
     }
-    pls.prefix[0] = 0;
-    for (int i = 0; i < pls.ndirs; i++) pls.prefix[i + 1] = pls.prefix[i] + pls.d[i].nchains;
+    for (sdr::PathLaunch* pl : {&pls, &plS}) {
+        pl->prefix[0] = 0;
+        for (int i = 0; i < pl->ndirs; i++) pl->prefix[i + 1] = pl->prefix[i] + pl->d[i].nchains;
+    }
     { KTimer kt(h, SDR_KERNEL_PATHS); sdr::launch_paths(g, pls, F, st); }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
-    sdr::WtaArgs wa{};
-    for (int p = 0; p < P; p++) wa.L[p] = Lr + (size_t)p * F * cells;
+    sdr::SouthWtaArgs wa{};
+    for (int p = 0; p < P - 1; p++) wa.L[p] = Lr + (size_t)p * F * cells;
     wa.npaths = P;
-    wa.cs_fstride = cells;
     wa.disp_raw = draw;
-    wa.disp_lr = dlr;
+    wa.keys2 = (uint32_t*)h->keys2.p;
     wa.disp_fstride = px;
     wa.uniq = e.uniq;
     wa.uniq_simd = e.uniq_simd;
-    wa.disp12MaxDiff = e.disp12MaxDiff;
-    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_wta_lr(g, wa, F, st); }
+    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
+    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st); }
     const bool speckle = e.speckle_ws > 0;
     { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, speckle ? dfin : dst, W, H, F, st); }
     if (speckle) {
@@ -418,7 +423,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin,
+    for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})

@@ -78,15 +78,24 @@ struct PathLaunch {
     PathDir d[kMaxPathDirs];
 };
 
-struct WtaArgs {
-    const int16_t* L[kMaxPaths];  // per-direction path costs [F][H][W1][D]
+// top-to-bottom direction fused with the WTA (sdr_paths.hip): the other P-1 directions' L in
+// sum order with the fused direction at position kSouthIdx
+constexpr int kSouthIdx = 2;  // summation order E, W, S, SE, SW, N, NE, NW
+// rows of slack after the cost volume and after the last path buffer: k_south_wta's loads run
+// up to this many rows past a chain's end instead of being clamped
+constexpr int kSouthPad = 48;
+struct SouthWtaArgs {
+    const int16_t* L[kMaxPaths];  // the P-1 other directions, in order, S removed
     int npaths;
-    size_t cs_fstride;
-    int16_t* disp_raw;   // WTA disparity before the LR check [F][H][W]
-    int16_t* disp_lr;    // after the LR check [F][H][W]
+    int16_t* disp_raw;   // [F][H][W] WTA disparity (invalid outside the matched columns)
+    uint32_t* keys2;     // [F][H][W] disp2 keys (minS << 16 | 0xffff - x)
     size_t disp_fstride;
-    int uniq, uniq_simd, disp12MaxDiff;
+    int uniq, uniq_simd;
 };
+void launch_south_wta(const Geometry& g, const PathLaunch& pl, const SouthWtaArgs& a, int F,
+                      hipStream_t st);
+void launch_lr_check(const Geometry& g, const int16_t* raw, const uint32_t* keys, int16_t* out,
+                     size_t fstride, int disp12MaxDiff, int F, hipStream_t st);
 
 void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st);
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
@@ -94,7 +103,6 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
-void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
 // src may equal dst; out_min (nullable) receives min over each output frame
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,

@@ -8,11 +8,13 @@
 // W1 steps at batch 1) overlap with the bandwidth-bound ones instead of running alone.
 // C loads are software-pipelined PF steps ahead with unconditional (clamped) addresses.
 //
-// k_wta_lr: one workgroup per image row: S = sat(sum_r L_r) per pixel, first-minimum WTA,
-// uniqueness test, subpixel fit, disp2 (right-view WTA by LDS atomicMin, ties -> largest x as in
-// OpenCV's descending loop) and the left-right check; fully parallel over pixels.
+// k_south_wta: the top-to-bottom chains fused with the winner-take-all (S = sat(sum_r L_r),
+// first minimum, uniqueness, subpixel, disp2 scatter); k_lr_check then applies the left-right
+// check per pixel.
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
+
+#include <algorithm>
 
 namespace sdr {
 
@@ -103,6 +105,37 @@ __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d,
     return ch;
 }
 
+// One step of the path recurrence on a wave's packed int16 pairs (lane l: disparities
+// [l*2K, l*2K + 2K)); Lp := L, delta2 := minL + P2 (both halves).
+template <int K, bool PAD>
+__device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
+                                             uint32_t P2x2, bool active) {
+    if constexpr (PAD) {
+#pragma unroll
+        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
+    }
+    const uint32_t up = lane_from_prev(Lp.r[K - 1], kMaxPair);
+    const uint32_t dn = lane_from_next(Lp.r[0], kMaxPair);
+    Regs<K> L;
+    uint32_t m = kMaxPair;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
+        const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
+        uint32_t t = pk_add_sat(pk_min(dm1, dp1), P1x2);
+        t = pk_min(pk_min(t, Lp.r[i]), delta2);
+        uint32_t l = pk_sub(pk_add(c.r[i], t), delta2);
+        if constexpr (PAD) l = active ? l : kMaxPair;
+        L.r[i] = l;
+        m = pk_min(m, l);
+    }
+    m = pk_min(m, funnel16(m, m));
+    m = wave_min_pk(m);
+    delta2 = pk_add(m, P2x2);
+    Lp = L;
+    return L;
+}
+
 template <int DPL, bool PAD, bool NT = false>
 __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     constexpr int K = DPL / 2;
@@ -144,31 +177,9 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
 
     auto step = [&](const int k, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
-        Regs<K> c = cring[j];
-        if constexpr (PAD) {
-#pragma unroll
-            for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
-        }
+        const Regs<K> c = cring[j];
         cring[j] = load_regs<K>(cptr(min(k + PF, last)));
-        const uint32_t up = lane_from_prev(Lp.r[K - 1], kMaxPair);
-        const uint32_t dn = lane_from_next(Lp.r[0], kMaxPair);
-        Regs<K> L;
-        uint32_t m = kMaxPair;
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
-            const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
-            uint32_t t = pk_add_sat(pk_min(dm1, dp1), P1x2);
-            t = pk_min(pk_min(t, Lp.r[i]), delta2);
-            uint32_t l = pk_sub(pk_add(c.r[i], t), delta2);
-            if constexpr (PAD) l = active ? l : kMaxPair;
-            L.r[i] = l;
-            m = pk_min(m, l);
-        }
-        m = pk_min(m, funnel16(m, m));
-        m = wave_min_pk(m);
-        delta2 = pk_add(m, P2x2);
-        Lp = L;
+        const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
         if (k >= ch.kwrite && active) {
             if constexpr (NT) store_regs_nt<K>(ob + (ptrdiff_t)k * pstep, L);
             else store_regs<K>(ob + (ptrdiff_t)k * pstep, L);
@@ -194,171 +205,305 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
     }
 }
 
+// Packed-int16 minimum over each 16-lane DPP row, broadcast within the row.
+__device__ __forceinline__ uint32_t row16_min_pk(uint32_t m) {
+    m = pk_min(m, dpp_mov<kDppQuadXor1>(m));
+    m = pk_min(m, dpp_mov<kDppQuadXor2>(m));
+    m = pk_min(m, dpp_mov<kDppRowHalfMirror>(m));
+    return pk_min(m, dpp_mov<kDppRowMirror>(m));
+}
+
 // ------------------------------------------------------------------------------------------
-// A.8 + A.9 fused: WTA / uniqueness / subpixel / disp2 / LR check, one workgroup per row.
-// A pixel's D path-cost sums live on a 16-lane DPP row (DPL disparities per lane), so one wave
-// instruction covers 4 pixels: each lane loads DPL*2 contiguous bytes per direction (16 B at
-// D = 128: a wave reads 1 KiB of consecutive pixels), and the argmin is a 4-step row reduction.
+// The top-to-bottom direction fused with A.8 (WTA / uniqueness / subpixel / disp2 scatter).
+//
+// One workgroup per column chain, two roles:
+//   wave 0 (producer) runs the serial recurrence of the chain (C prefetched kSouthPFP rows
+//     ahead) and stages each row's L in LDS, kSouthRB rows per block, two blocks double-buffered;
+//   waves 1..3 (consumers) each own 4 rows of a block: a pixel's D disparities sit on one 16-lane
+//     DPP row (4 pixels per wave instruction, 16 B per lane per direction), the other P-1
+//     directions' L are read from HBM (prefetched whole blocks ahead), the staged L is added from
+//     LDS, and the winner-take-all runs on the saturated sums.
+// A block is handed over by one barrier.  The serial chain is the only latency-bound part and
+// it does nothing but the recurrence; the WTA and the HBM reads of the other directions run on
+// three more waves beside it.  L of this direction is never written to HBM, so the pass moves
+// 2 + 2(P-1) B/cell.  The uniqueness test needs only the smallest S[d] with |d - best| > 1 (both
+// of OpenCV's rules are monotone in S[d]): a masked packed minimum.  disp2 (right-view WTA) is a
+// global atomicMin per pixel on (minS << 16 | 0xffff - x) keys (ties -> largest x, OpenCV's
+// descending loop); k_lr_check applies A.9.  Loads run past a chain's end into the buffers'
+// kSouthPad rows of slack instead of being clamped.
 // ------------------------------------------------------------------------------------------
-constexpr int kWtaWaves = 4;   // 4 workgroups/CU at <= 128 VGPRs: 720 rows resident in one pass
-constexpr int kWtaGL = 16;     // lanes per pixel
-constexpr int kWtaPPW = 4;     // pixels per wave instruction
+// 1 producer + 3 consumer waves (256 threads): at <= 96 VGPRs five workgroups fit a CU, so
+// the 1152 column chains of a 1280x720 d=128 frame are resident in one pass
+constexpr int kSouthConsumers = 3;
+constexpr int kSouthRB = 4 * kSouthConsumers;  // rows per block (4 per consumer wave)
+constexpr int kSouthPFP = 2 * kSouthRB;        // producer prefetch distance in rows (two blocks)
 
 template <int DPL, bool PAD, int NP>
-__global__ __launch_bounds__(64 * kWtaWaves) void k_wta_lr(Geometry g, WtaArgs a) {
+__global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g, PathLaunch pl,
+                                                                           SouthWtaArgs a) {
     constexpr int K = DPL / 2;
-    // directions x pairs x in-flight iterations held in registers: keep the ring near 64 VGPRs
-    constexpr int PF = (NP * K <= 16) ? 4 : (NP * K <= 24 ? 3 : 2);
-    extern __shared__ int wsm[];
-    const int W = g.W, W1 = g.W1, D = g.D;
-    uint32_t* keys = (uint32_t*)wsm;   // [W]
-    int* disp2 = wsm + W;              // [W]
-    int* drow = wsm + 2 * W;           // [W]
-    const int y = blockIdx.x, f = blockIdx.y;
-    const int lane = threadIdx.x & 63, gl = lane & (kWtaGL - 1), grp = lane >> 4;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t kInit = 32767u << 16;
-    const int invalid = (g.minD - 1) * 16;
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        keys[x] = kInit;
-        drow[x] = invalid;
+    constexpr int RB = kSouthRB, PFP = kSouthPFP;
+    static_assert(PFP == 2 * RB, "the producer ring spans two row blocks");
+    static_assert(PFP + RB <= kSouthPad, "prefetch overrun must fit the buffers' row slack");
+    constexpr int WDPL = DPL * 4;  // consumer: disparities per lane
+    constexpr int WK = WDPL / 2;
+    constexpr int DMAX = 64 * DPL;
+    constexpr int LSTR = DMAX / 2 + 4;  // dwords per staged row (padded: rows of a wave's 4 pixels)
+    // consumer prefetch distance in blocks: the ring of the other directions' L within ~32 VGPRs
+    constexpr int PD = NP * WK <= 8 ? 3 : (NP * WK <= 16 ? 2 : 1);
+    __shared__ uint32_t sL[2][RB][LSTR];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int cg = blockIdx.x;
+    const int f = blockIdx.y;
+    int di = 0;
+    while (cg >= pl.prefix[di + 1]) di++;
+    const PathDir pd = pl.d[di];
+    const Chain ch = make_chain(g, pd, cg - pl.prefix[di]);
+    if (ch.len <= 0) return;  // whole workgroup
+    const int D = g.D, W1 = g.W1;
+    const ptrdiff_t pstep = (ptrdiff_t)W1 * D;
+    const size_t p0 = (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D;
+    const int last = ch.len - 1;
+    const int nblk = (ch.len + RB - 1) / RB;
+
+    if (wv == 0) {
+        // ---------------- producer: the recurrence, L rows to LDS ----------------
+        __builtin_amdgcn_s_setprio(2);
+        const bool active = !PAD || lane * DPL < D;
+        // addresses = wave-uniform row base (SGPRs, scalar arithmetic) + 32-bit lane byte offset
+        const uint32_t lofs = (uint32_t)((PAD ? min(lane, D / DPL - 1) : lane) * DPL * 2);
+        const char* cbase = (const char*)(pl.C + p0);
+        // 3WAY stripes: a chain starting at aux_row0 reads stripe-local cost rows first
+        const int naux = pd.Caux ? pd.aux_rows : 0;
+        const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D) : cbase;
+        const ptrdiff_t rowb = pstep * 2;
+        auto cload = [&](int k) __attribute__((always_inline)) {
+            const char* base = (k < naux ? abase : cbase) + (ptrdiff_t)k * rowb;
+            return load_regs<K>((const int16_t*)(base + lofs));
+        };
+        Regs<K> cring[PFP];
+#pragma unroll
+        for (int j = 0; j < PFP; j++) cring[j] = cload(j);
+        Regs<K> Lp;
+#pragma unroll
+        for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
+        const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
+        uint32_t delta2 = P2x2;
+        // ring slot j = k % PFP; LDS slot = block parity = j / RB
+        auto step = [&](const int k, auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            const Regs<K> c = cring[j];
+            cring[j] = cload(k + PFP);
+            const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
+#pragma unroll
+            for (int i = 0; i < K; i++) sL[j / RB][j % RB][lane * K + i] = L.r[i];
+        };
+        auto step_hi = [&](const int k, auto jc) __attribute__((always_inline)) {
+            step(k, std::integral_constant<int, decltype(jc)::value + RB>{});
+        };
+        int b = 0;
+        for (; b + 2 <= nblk; b += 2) {
+            unroll_rows(step, b * RB, std::make_integer_sequence<int, RB>{});
+            __syncthreads();
+            unroll_rows(step_hi, b * RB + RB, std::make_integer_sequence<int, RB>{});
+            __syncthreads();
+        }
+        if (b < nblk) {
+            unroll_rows(step, b * RB, std::make_integer_sequence<int, RB>{});
+            __syncthreads();
+        }
+        __syncthreads();  // the consumers' last block
+        return;
     }
-    __syncthreads();
 
-    const bool active = !PAD || gl * DPL < D;
-    const int d0 = (PAD ? min(gl, D / DPL - 1) : gl) * DPL;  // padding lanes re-read the last word
-    const size_t rowoff = (size_t)f * a.cs_fstride + (size_t)y * W1 * D + d0;
-    const bool check_uniq = a.uniq > 0 || !a.uniq_simd;
-    const int uniq_simd = a.uniq_simd ? 1 : 0;
-    const int lhs_scale = 100 - a.uniq;
-    // trunc((double)n * inv100u) == n / (100-u) for 0 <= n < 2^22
-    const double inv100u = 1.0 / (double)(100 - a.uniq) * (1.0 + 0x1p-40);
-    const int16_t* Lp[NP];
-#pragma unroll
-    for (int p = 0; p < NP; p++) Lp[p] = a.L[p] + rowoff;
-
-    // iteration t of this wave covers pixels xw(t) .. xw(t)+3, pixel xw(t)+grp on this lane
-    const int nit = (W1 + kWtaPPW * kWtaWaves - 1) / (kWtaPPW * kWtaWaves);
-    auto xw = [&](int t) { return (t * kWtaWaves + wave) * kWtaPPW; };
-    auto load_px = [&](int t, Regs<K>* dst) __attribute__((always_inline)) {
-        const size_t o = (size_t)min(xw(t) + grp, W1 - 1) * D;
-#pragma unroll
-        for (int p = 0; p < NP; p++) dst[p] = load_regs<K>(Lp[p] + o);
+    // ---------------- consumers: the other directions + WTA, 4 rows per wave ----------------
+    const int gl = lane & 15, grp = lane >> 4;
+    const int r = (wv - 1) * 4 + grp;  // this lane group's row within a block
+    const bool wactive = !PAD || gl * WDPL < D;
+    const int wd0 = (PAD ? min(gl, D / WDPL - 1) : gl) * WDPL;
+    // addresses = wave-uniform block base (SGPRs) + 32-bit lane byte offset (row r, disparity wd0)
+    const ptrdiff_t bstepb = (ptrdiff_t)RB * pstep * 2;
+    const uint32_t lofs = (uint32_t)(((size_t)r * pstep + wd0) * 2);
+    auto oload = [&](int q, int blk) __attribute__((always_inline)) {
+        const char* base = (const char*)(a.L[q] + p0) + (ptrdiff_t)blk * bstepb;
+        return load_regs<WK>((const int16_t*)(base + lofs));
     };
+    // rows before kw belong to the previous 3WAY stripe: recurred through, never output
+    const int kw = ch.kwrite;
+    const int invalid = (g.minD - 1) * 16;
+    const bool check_uniq = a.uniq > 0 || !a.uniq_simd;
+    const bool uniq_simd = a.uniq_simd != 0;
+    const int lhs_scale = 100 - a.uniq;
+    const double inv100u = 1.0 / (double)(100 - a.uniq) * (1.0 + 0x1p-40);
+    const int x = ch.x0;  // matched-range column of this chain
+    int16_t* raw = a.disp_raw + (size_t)f * a.disp_fstride + x + g.minX1;
+    uint32_t* keys = a.keys2 + (size_t)f * a.disp_fstride;
 
-    Regs<K> ring[PF][NP];
+    Regs<WK> oring[PD][NP];
 #pragma unroll
-    for (int s = 0; s < PF; s++) load_px(s, ring[s]);
+    for (int s = 0; s < PD; s++) {
+        if (s < nblk) {
+#pragma unroll
+            for (int q = 0; q < NP; q++) oring[s][q] = oload(q, s);
+        }
+    }
 
-    auto iter = [&](const int t, auto sc) __attribute__((always_inline)) {
+    auto consume = [&](const int b, auto sc) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
-        Regs<K> St = ring[s][0];
+        Regs<WK> o[NP];
 #pragma unroll
-        for (int p = 1; p < NP; p++)
+        for (int q = 0; q < NP; q++) o[q] = oring[s][q];
+        if (b + PD < nblk) {
 #pragma unroll
-            for (int i = 0; i < K; i++) St.r[i] = pk_add_sat(St.r[i], ring[s][p].r[i]);
-        load_px(t + PF, ring[s]);
-        const int x = xw(t) + grp;
+            for (int q = 0; q < NP; q++) oring[s][q] = oload(q, b + PD);
+        }
+        // S = sat(sum of the P path costs), the fused direction's L from LDS
+        const uint32_t* ls = &sL[b & 1][r][wd0 / 2];
+        Regs<WK> St;
+#pragma unroll
+        for (int i = 0; i < WK; i++) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int p = 0; p <= NP; p++) {
+                const uint32_t v = p == kSouthIdx ? ls[i] : o[p < kSouthIdx ? p : p - 1].r[i];
+                acc = p == 0 ? v : pk_add_sat(acc, v);
+            }
+            St.r[i] = acc;
+        }
+        const int k = b * RB + r;
+        const bool rowok = k >= kw && k <= last;
+        // first minimum: packed (S + 32768) << 16 | d keys, min over the 16-lane row
         uint32_t key = 0xffffffffu;
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-            const uint32_t d = (uint32_t)(gl * DPL + 2 * i);
+        for (int i = 0; i < WK; i++) {
+            const uint32_t d = (uint32_t)(gl * WDPL + 2 * i);
             const uint32_t lo = (uint32_t)((int)(short)(St.r[i] & 0xffff) + 32768);
             const uint32_t hi = (uint32_t)((int)(short)(St.r[i] >> 16) + 32768);
             key = min(key, min((lo << 16) | d, (hi << 16) | (d + 1)));
         }
-        key = row16_min_u32(active ? key : 0xffffffffu);
+        key = row16_min_u32(wactive ? key : 0xffffffffu);
         const int minS = (int)(key >> 16) - 32768;
         const int best = (int)(key & 0xffff);
-        // uniqueness: reject if some d with |d-best| > 1 has S[d]*(100-u) < minS*100 (scalar
-        // rule) or S[d] < (short)(thresh+1), thresh = (100*minS)/(100-u) (SIMD rule)
-        const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);
-        const int rhs = minS * 100;
-        int bad = 0;
+        // uniqueness: min of S[d] over |d - best| > 1 (0 <= S <= 32767: or-ing 0x7fff masks a half)
+        uint32_t m2 = kMaxPair;
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int d = gl * DPL + 2 * i + h;
-                const int v = (int)(short)(h ? (St.r[i] >> 16) : (St.r[i] & 0xffff));
-                const int cs = (v < thr16) & uniq_simd;
-                const int cc = (v * lhs_scale < rhs) & (uniq_simd ^ 1);
-                bad |= (cs | cc) & (abs(d - best) > 1);
-            }
+        for (int i = 0; i < WK; i++) {
+            const int t = gl * WDPL + 2 * i - best;
+            const uint32_t mk = ((unsigned)(t + 1) <= 2u ? 0x7fffu : 0u) | ((unsigned)(t + 2) <= 2u ? 0x7fff0000u : 0u);
+            m2 = pk_min(m2, St.r[i] | mk);
         }
-        bad &= (int)active & (int)check_uniq;
-        const bool reject = ((__ballot(bad != 0) >> (16 * grp)) & 0xffffull) != 0;
+        m2 = wactive ? m2 : kMaxPair;
+        m2 = pk_min(m2, funnel16(m2, m2));
+        m2 = row16_min_pk(m2);
+        const int min2 = (int)(m2 & 0x7fff);
+        // SIMD rule: S[d] < (short)(thresh + 1), thresh = (100*minS)/(100-u); scalar: S*(100-u) < 100*minS
+        const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);
+        const bool reject = check_uniq && (uniq_simd ? (min2 < thr16) : (min2 * lhs_scale < minS * 100));
         // subpixel: d*16 + ((S[d-1]-S[d+1])*16 + den) / (2*den), C truncating division
         const int dm = max(best - 1, 0), dp = min(best + 1, D - 1);
         uint32_t wm = St.r[0], wp = St.r[0];
 #pragma unroll
-        for (int i = 1; i < K; i++) {
-            if (((dm % DPL) >> 1) == i) wm = St.r[i];
-            if (((dp % DPL) >> 1) == i) wp = St.r[i];
+        for (int i = 1; i < WK; i++) {
+            if (((dm % WDPL) >> 1) == i) wm = St.r[i];
+            if (((dp % WDPL) >> 1) == i) wp = St.r[i];
         }
-        const uint32_t am = (uint32_t)__shfl((int)wm, grp * kWtaGL + dm / DPL);
-        const uint32_t ap = (uint32_t)__shfl((int)wp, grp * kWtaGL + dp / DPL);
-        const int Sm = (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
-        const int Sp = (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
-        const int den = max(Sm + Sp - 2 * minS, 1);
-        const int q = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
-        const int d16 = best * 16 + (((0 < best) & (best < D - 1)) ? q : 0);
-        if (gl == 0 && !reject && x < W1) {
-            drow[x + g.minX1] = d16 + g.minD * 16;
-            const int x2 = x + g.minX1 - best - g.minD;
-            if (x2 >= 0 && x2 < W) atomicMin(&keys[x2], ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+        const uint32_t am = (uint32_t)__shfl((int)wm, grp * 16 + dm / WDPL);
+        const uint32_t ap = (uint32_t)__shfl((int)wp, grp * 16 + dp / WDPL);
+        if (gl == 0 && rowok) {
+            const size_t y = (size_t)(ch.y0 + k);
+            int out = invalid;
+            if (!reject) {
+                const int Sm = (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
+                const int Sp = (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
+                const int den = max(Sm + Sp - 2 * minS, 1);
+                const int qq = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
+                out = best * 16 + (((0 < best) & (best < D - 1)) ? qq : 0) + g.minD * 16;
+                const int x2 = x + g.minX1 - best - g.minD;
+                if (x2 >= 0 && x2 < g.W)
+                    atomicMin(&keys[y * g.W + x2], ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+            }
+            raw[y * g.W] = (int16_t)out;
         }
     };
-    int t = 0;
-    for (; t + PF <= nit; t += PF) unroll_rows(iter, t, std::make_integer_sequence<int, PF>{});
-    unroll_rows_tail(iter, t, nit - 1, std::make_integer_sequence<int, PF - 1>{});
-    __syncthreads();
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        const uint32_t k = keys[x];
-        disp2[x] = k == kInit ? invalid : ((0xffff - (int)(k & 0xffff)) + g.minX1 - x);
+    auto consume_sync = [&](const int b, auto sc) __attribute__((always_inline)) {
+        consume(b, sc);
+        __syncthreads();
+    };
+    __syncthreads();  // block 0 staged
+    int b = 0;
+    for (; b + PD <= nblk; b += PD) unroll_rows(consume_sync, b, std::make_integer_sequence<int, PD>{});
+    unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, PD - 1>{});
+}
+
+// disp_raw := invalid, keys2 := no match (per frame, before k_south_wta)
+__global__ __launch_bounds__(256) void k_wta_init(int16_t* __restrict__ raw, uint32_t* __restrict__ keys,
+                                                  size_t n, int invalid) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        raw[i] = (int16_t)invalid;
+        keys[i] = 32767u << 16;
     }
-    __syncthreads();
-    int16_t* raw = a.disp_raw + (size_t)f * a.disp_fstride + (size_t)y * W;
-    int16_t* out = a.disp_lr + (size_t)f * a.disp_fstride + (size_t)y * W;
-    const int maxX1 = g.minX1 + W1;
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        int d1 = drow[x];
-        raw[x] = (int16_t)d1;
-        if (x >= g.minX1 && x < maxX1 && d1 != invalid) {
-            const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
-            const int _x = x - _d, x_ = x - d_;
-            if (0 <= _x && _x < W && disp2[_x] >= g.minD && abs(disp2[_x] - _d) > a.disp12MaxDiff &&
-                0 <= x_ && x_ < W && disp2[x_] >= g.minD && abs(disp2[x_] - d_) > a.disp12MaxDiff)
+}
+
+// A.9 on the fused pass's outputs: disp2 from the scattered keys, then OpenCV's check
+__global__ __launch_bounds__(256) void k_lr_check(Geometry g, const int16_t* __restrict__ raw,
+                                                  const uint32_t* __restrict__ keys,
+                                                  int16_t* __restrict__ out, size_t fstride,
+                                                  int disp12MaxDiff) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y, f = blockIdx.z;
+    if (x >= g.W) return;
+    const size_t ro = (size_t)f * fstride + (size_t)y * g.W;
+    const int invalid = (g.minD - 1) * 16;
+    const uint32_t kInit = 32767u << 16;
+    auto disp2 = [&](int xx) {
+        const uint32_t k = keys[ro + xx];
+        return k == kInit ? invalid : ((0xffff - (int)(k & 0xffff)) + g.minX1 - xx);
+    };
+    int d1 = raw[ro + x];
+    if (x >= g.minX1 && x < g.minX1 + g.W1 && d1 != invalid) {
+        const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+        const int _x = x - _d, x_ = x - d_;
+        if (0 <= _x && _x < g.W && 0 <= x_ && x_ < g.W) {
+            const int a2 = disp2(_x), b2 = disp2(x_);
+            if (a2 >= g.minD && abs(a2 - _d) > disp12MaxDiff && b2 >= g.minD && abs(b2 - d_) > disp12MaxDiff)
                 d1 = invalid;
         }
-        out[x] = (int16_t)d1;
     }
+    out[ro + x] = (int16_t)d1;
 }
 
 template <int DPL, bool PAD>
-static void launch_wta_np(const Geometry& g, const WtaArgs& a, int F, hipStream_t st) {
-    dim3 grid(g.H, F);
-    const size_t lds = (size_t)3 * g.W * 4;
-    const dim3 block(64 * kWtaWaves);
+static void launch_south_np(const Geometry& g, const PathLaunch& pl, const SouthWtaArgs& a, int F,
+                            hipStream_t st) {
+    dim3 grid(pl.prefix[pl.ndirs], F);
+    dim3 block(64 * (1 + kSouthConsumers));
     switch (a.npaths) {
-    case 3: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 3>), grid, block, lds, st, g, a); break;
-    case 5: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 5>), grid, block, lds, st, g, a); break;
-    default: hipLaunchKernelGGL((k_wta_lr<DPL, PAD, 8>), grid, block, lds, st, g, a); break;
+    case 3: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 2>), grid, block, 0, st, g, pl, a); break;
+    case 5: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 4>), grid, block, 0, st, g, pl, a); break;
+    default: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 7>), grid, block, 0, st, g, pl, a); break;
     }
 }
 
-void launch_wta_lr(const Geometry& g, const WtaArgs& a, int F, hipStream_t st) {
-    // DPL = disparities per lane so that a pixel fits one 16-lane row
-    if (g.D <= 64) {
-        if (g.D < 64) launch_wta_np<4, true>(g, a, F, st);
-        else launch_wta_np<4, false>(g, a, F, st);
-    } else if (g.D <= 128) {
-        if (g.D < 128) launch_wta_np<8, true>(g, a, F, st);
-        else launch_wta_np<8, false>(g, a, F, st);
+void launch_south_wta(const Geometry& g, const PathLaunch& pl, const SouthWtaArgs& a, int F,
+                      hipStream_t st) {
+    const size_t n = (size_t)F * a.disp_fstride;
+    hipLaunchKernelGGL(k_wta_init, dim3((unsigned)std::min<size_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                       st, a.disp_raw, a.keys2, n, (g.minD - 1) * 16);
+    if (pl.prefix[pl.ndirs] <= 0) return;
+    if (g.D <= 128) {
+        if (g.D < 128) launch_south_np<2, true>(g, pl, a, F, st);
+        else launch_south_np<2, false>(g, pl, a, F, st);
     } else {
-        if (g.D < 256) launch_wta_np<16, true>(g, a, F, st);
-        else launch_wta_np<16, false>(g, a, F, st);
+        if (g.D < 256) launch_south_np<4, true>(g, pl, a, F, st);
+        else launch_south_np<4, false>(g, pl, a, F, st);
     }
+}
+
+void launch_lr_check(const Geometry& g, const int16_t* raw, const uint32_t* keys, int16_t* out,
+                     size_t fstride, int disp12MaxDiff, int F, hipStream_t st) {
+    hipLaunchKernelGGL(k_lr_check, dim3((g.W + 255) / 256, g.H, F), dim3(256), 0, st, g, raw, keys, out,
+                       fstride, disp12MaxDiff);
 }
 
 }  // namespace sdr

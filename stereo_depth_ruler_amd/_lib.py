@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsdr.so")
+# SDR_LIB_VARIANT selects an in-tree experiment build lib/libsdr-<variant>.so (scripts/exp_*.sh)
+_VARIANT = os.environ.get("SDR_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, "lib", f"libsdr-{_VARIANT}.so" if _VARIANT else "libsdr.so")
 
 SDR_OK = 0
 ERRORS = {

@@ -35,17 +35,20 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_native(force: bool = False, verbose: bool = False) -> str:
+def build_native(force: bool = False, verbose: bool = False, variant: str = "",
+                 defines: tuple = ()) -> str:
     """Compiles each HIP source to an object in parallel (relocatable device code is not needed:
-    every kernel is launched from the file that defines it), then links the shared library."""
-    if not force and not _stale():
+    every kernel is launched from the file that defines it), then links the shared library.
+    variant/defines: an experiment build lib/libsdr-<variant>.so with extra -D switches."""
+    out = OUT if not variant else os.path.join(os.path.dirname(OUT), f"libsdr-{variant}.so")
+    if not variant and not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    objdir = os.path.join(os.path.dirname(OUT), "obj")
+    objdir = os.path.join(os.path.dirname(OUT), "obj" + (f"-{variant}" if variant else ""))
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              "-Wall", "-Wno-unused-function", "-Wno-unused-result",
-             "-I", os.path.join(ROOT, "include")]
+             "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines]
     hipcc = _hipcc()
     objs, procs = [], []
     for f in SOURCES:
@@ -58,13 +61,19 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     failed = [cmd for cmd, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT + ".tmp"]
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(link))
     subprocess.check_call(link)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build_native(force=True, verbose=True))
+    import sys
+
+    # python build.py [variant -DNAME=V ...]
+    if len(sys.argv) > 1:
+        print(build_native(force=True, variant=sys.argv[1], defines=tuple(a[2:] for a in sys.argv[2:])))
+    else:
+        print(build_native(force=True, verbose=True))

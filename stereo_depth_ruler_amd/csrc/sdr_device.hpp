@@ -94,12 +94,21 @@ __device__ __forceinline__ uint32_t wave_min_pk(uint32_t m) {
     return pk_min(p32[0], p32[1]);
 }
 
-// Unsigned 32-bit minimum over all 64 lanes, broadcast.
+// min(v, v from the DPP-permuted lane) as ONE v_min_u32_dpp: the identity (all ones) as the
+// update's old value lets the compiler fold the DPP move into the min.
+template <int CTRL>
+__device__ __forceinline__ uint32_t min_u32_dpp(uint32_t v) {
+    const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)v, CTRL, 0xf, 0xf, false);
+    return min(v, t);
+}
+
+// Unsigned 32-bit minimum over all 64 lanes, broadcast.  Also the minimum of packed non-negative
+// int16 pairs whose two halves are equal (u32 order = int16 order there).
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
-    m = min(m, dpp_mov<kDppQuadXor1>(m));
-    m = min(m, dpp_mov<kDppQuadXor2>(m));
-    m = min(m, dpp_mov<kDppRowHalfMirror>(m));
-    m = min(m, dpp_mov<kDppRowMirror>(m));
+    m = min_u32_dpp<kDppQuadXor1>(m);
+    m = min_u32_dpp<kDppQuadXor2>(m);
+    m = min_u32_dpp<kDppRowHalfMirror>(m);
+    m = min_u32_dpp<kDppRowMirror>(m);
     auto p16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
     m = min((uint32_t)p16[0], (uint32_t)p16[1]);
     auto p32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
@@ -108,10 +117,10 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
 
 // Unsigned 32-bit minimum over each 16-lane DPP row, broadcast within the row.
 __device__ __forceinline__ uint32_t row16_min_u32(uint32_t m) {
-    m = min(m, dpp_mov<kDppQuadXor1>(m));
-    m = min(m, dpp_mov<kDppQuadXor2>(m));
-    m = min(m, dpp_mov<kDppRowHalfMirror>(m));
-    return min(m, dpp_mov<kDppRowMirror>(m));
+    m = min_u32_dpp<kDppQuadXor1>(m);
+    m = min_u32_dpp<kDppQuadXor2>(m);
+    m = min_u32_dpp<kDppRowHalfMirror>(m);
+    return min_u32_dpp<kDppRowMirror>(m);
 }
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }

@@ -69,6 +69,57 @@ __device__ __forceinline__ void store_regs(int16_t* p, const Regs<K>& v) {
     }
 }
 
+// Buffer-resource access: the row base lives in a wave-uniform resource descriptor (SGPRs, scalar
+// arithmetic), the lane's byte offset in one VGPR, so a load or store costs no vector address math.
+#ifndef SDR_PATHS_BUF
+#define SDR_PATHS_BUF 1  // k_paths through buffer resources (0: flat global addresses)
+#endif
+#ifndef SDR_SOUTH_BUF
+#define SDR_SOUTH_BUF 1  // k_south_wta through buffer resources (0: flat global addresses)
+#endif
+using Rsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ Rsrc rsrc_at(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+template <int K>
+__device__ __forceinline__ Regs<K> load_buf(Rsrc r, uint32_t vofs) {
+    Regs<K> v;
+    if constexpr (K == 1) {
+        v.r[0] = __builtin_amdgcn_raw_buffer_load_b32(r, vofs, 0, 0);
+    } else if constexpr (K == 2) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, vofs, 0, 0);
+        v.r[0] = t[0];
+        v.r[1] = t[1];
+    } else {
+        static_assert(K % 4 == 0, "K = 1, 2 or a multiple of 4");
+#pragma unroll
+        for (int j = 0; j < K / 4; j++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, vofs + 16 * j, 0, 0);
+            v.r[4 * j] = t[0]; v.r[4 * j + 1] = t[1]; v.r[4 * j + 2] = t[2]; v.r[4 * j + 3] = t[3];
+        }
+    }
+    return v;
+}
+
+// non-temporal (aux = nt) stores of K packed pairs
+template <int K>
+__device__ __forceinline__ void store_buf_nt(Rsrc r, uint32_t vofs, const Regs<K>& v) {
+    if constexpr (K == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(v.r[0], r, vofs, 0, 2);
+    } else if constexpr (K == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) uint32_t){v.r[0], v.r[1]}, r,
+                                              vofs, 0, 2);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K / 4; j++)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (__attribute__((ext_vector_type(4))) uint32_t){v.r[4 * j], v.r[4 * j + 1], v.r[4 * j + 2],
+                                                               v.r[4 * j + 3]},
+                r, vofs + 16 * j, 0, 2);
+    }
+}
+
 struct Chain {
     int x0, y0, dx, dy, len, kwrite;
 };
@@ -129,8 +180,9 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
         L.r[i] = l;
         m = pk_min(m, l);
     }
+    // both halves := min of the pair; L >= 0, so the u32 order of such words is the int16 order
     m = pk_min(m, funnel16(m, m));
-    m = wave_min_pk(m);
+    m = wave_min_u32(m);
     delta2 = pk_add(m, P2x2);
     Lp = L;
     return L;
@@ -153,21 +205,26 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
 
     const int D = g.D, W1 = g.W1;
     const bool active = !PAD || lane * DPL < D;
+    // addresses = wave-uniform base (SGPRs, scalar arithmetic) + 32-bit lane byte offset;
     // inactive (padding) lanes read the pixel's last word and discard it
-    const int loff = (PAD ? min(lane, D / DPL - 1) : lane) * DPL;
-    const ptrdiff_t pstep = (ptrdiff_t)(ch.dy * W1 + ch.dx) * D;
-    const size_t p0 = ((size_t)ch.y0 * W1 + ch.x0) * D;
-    const int16_t* cb = pl.C + (size_t)f * pl.cs_fstride + p0 + loff;
-    int16_t* ob = pd.out + (size_t)f * pl.cs_fstride + p0 + loff;
+    const uint32_t lofs = (uint32_t)((PAD ? min(lane, D / DPL - 1) : lane) * DPL * 2);
+    const ptrdiff_t rowb = (ptrdiff_t)(ch.dy * W1 + ch.dx) * D * 2;
+    const size_t p0 = (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D;
+    const char* cbase = (const char*)(pl.C + p0);
+    char* obase = (char*)(pd.out + p0);
     // 3WAY stripes: a DIR_S chain starting at aux_row0 reads stripe-local cost rows first
     const int naux = pd.Caux ? pd.aux_rows : 0;
-    const int16_t* ab = pd.Caux ? pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D + loff : cb;
+    const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D) : cbase;
     const int last = ch.len - 1;
-    auto cptr = [&](int k) -> const int16_t* { return (k < naux ? ab : cb) + (ptrdiff_t)k * pstep; };
+    auto cload = [&](int k) __attribute__((always_inline)) {
+        const char* base = (k < naux ? abase : cbase) + (ptrdiff_t)k * rowb;
+        if constexpr (SDR_PATHS_BUF) return load_buf<K>(rsrc_at(base), lofs);
+        else return load_regs<K>((const int16_t*)(base + lofs));
+    };
 
     Regs<K> cring[PF];
 #pragma unroll
-    for (int j = 0; j < PF; j++) cring[j] = load_regs<K>(cptr(min(j, last)));
+    for (int j = 0; j < PF; j++) cring[j] = cload(min(j, last));
 
     Regs<K> Lp;
 #pragma unroll
@@ -178,11 +235,12 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     auto step = [&](const int k, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const Regs<K> c = cring[j];
-        cring[j] = load_regs<K>(cptr(min(k + PF, last)));
+        cring[j] = cload(min(k + PF, last));
         const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
         if (k >= ch.kwrite && active) {
-            if constexpr (NT) store_regs_nt<K>(ob + (ptrdiff_t)k * pstep, L);
-            else store_regs<K>(ob + (ptrdiff_t)k * pstep, L);
+            if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(obase + (ptrdiff_t)k * rowb), lofs, L);
+            else if constexpr (NT) store_regs_nt<K>((int16_t*)(obase + (ptrdiff_t)k * rowb + lofs), L);
+            else store_regs<K>((int16_t*)(obase + (ptrdiff_t)k * rowb + lofs), L);
         }
     };
     int k0 = 0;
@@ -203,14 +261,6 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
         if (g.D < 256) hipLaunchKernelGGL((k_paths<4, true, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<4, false, true>), grid, dim3(256), 0, st, g, pl);
     }
-}
-
-// Packed-int16 minimum over each 16-lane DPP row, broadcast within the row.
-__device__ __forceinline__ uint32_t row16_min_pk(uint32_t m) {
-    m = pk_min(m, dpp_mov<kDppQuadXor1>(m));
-    m = pk_min(m, dpp_mov<kDppQuadXor2>(m));
-    m = pk_min(m, dpp_mov<kDppRowHalfMirror>(m));
-    return pk_min(m, dpp_mov<kDppRowMirror>(m));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -280,7 +330,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         const ptrdiff_t rowb = pstep * 2;
         auto cload = [&](int k) __attribute__((always_inline)) {
             const char* base = (k < naux ? abase : cbase) + (ptrdiff_t)k * rowb;
-            return load_regs<K>((const int16_t*)(base + lofs));
+            if constexpr (SDR_SOUTH_BUF) return load_buf<K>(rsrc_at(base), lofs);
+            else return load_regs<K>((const int16_t*)(base + lofs));
         };
         Regs<K> cring[PFP];
 #pragma unroll
@@ -327,7 +378,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     const uint32_t lofs = (uint32_t)(((size_t)r * pstep + wd0) * 2);
     auto oload = [&](int q, int blk) __attribute__((always_inline)) {
         const char* base = (const char*)(a.L[q] + p0) + (ptrdiff_t)blk * bstepb;
-        return load_regs<WK>((const int16_t*)(base + lofs));
+        if constexpr (SDR_SOUTH_BUF) return load_buf<WK>(rsrc_at(base), lofs);
+        else return load_regs<WK>((const int16_t*)(base + lofs));
     };
     // rows before kw belong to the previous 3WAY stripe: recurred through, never output
     const int kw = ch.kwrite;
@@ -395,7 +447,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         }
         m2 = wactive ? m2 : kMaxPair;
         m2 = pk_min(m2, funnel16(m2, m2));
-        m2 = row16_min_pk(m2);
+        m2 = row16_min_u32(m2);
         const int min2 = (int)(m2 & 0x7fff);
         // SIMD rule: S[d] < (short)(thresh + 1), thresh = (100*minS)/(100-u); scalar: S*(100-u) < 100*minS
         const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);

@@ -20,7 +20,7 @@ def case(h, w, D, mode, bs=5, minD=0, uniq=12, sp=(0, 0), d12=1, seed=0, P=(600,
     tg = time.time() - t
     p = O.make_params(*args)
     w1 = w + min(minD, 0) - max(minD + D, 0)
-    C_g = m.debug_stage(0, (h, w1, D), np.int16)
+    C_g = m.debug_cost_volume(h, w1, D)
     lr_g = m.debug_stage(2, (h, w), np.int16)
     res = {}
     if mode != 2:

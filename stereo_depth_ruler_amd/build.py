@@ -72,8 +72,9 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
 if __name__ == "__main__":
     import sys
 
-    # python build.py [variant -DNAME=V ...]
+    # python build.py [variant NAME=V ...]  (-DNAME=V accepted too)
     if len(sys.argv) > 1:
-        print(build_native(force=True, variant=sys.argv[1], defines=tuple(a[2:] for a in sys.argv[2:])))
+        defs = tuple(a[2:] if a.startswith("-D") else a for a in sys.argv[2:])
+        print(build_native(force=True, variant=sys.argv[1], defines=defs))
     else:
         print(build_native(force=True, verbose=True))

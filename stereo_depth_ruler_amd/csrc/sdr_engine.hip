@@ -141,6 +141,7 @@ struct sdr_sgbm {
     std::vector<hipEvent_t> kev;
     std::vector<int> kkind;
     size_t kused = 0;
+    size_t path_slack = 0;  // elements of slack in front of C and Lr (last compute)
 };
 
 namespace {
@@ -229,9 +230,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
 
     if ((rc = ensure(h->planesL, F * 3 * px * 8))) return rc;
     if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
-    const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;  // k_south_wta's load overrun
-    if ((rc = ensure(h->C, (F * cells + slack) * 2))) return rc;
-    if ((rc = ensure(h->Lr, ((size_t)(P - 1) * F * cells + slack) * 2))) return rc;
+    // the path kernels' loads overrun a chain's ends by up to kSouthPad rows: slack both sides
+    const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
+    if ((rc = ensure(h->C, (F * cells + 2 * slack) * 2))) return rc;
+    if ((rc = ensure(h->Lr, ((size_t)(P - 1) * F * cells + 2 * slack) * 2))) return rc;
     if ((rc = ensure(h->keys2, F * px * 4))) return rc;
     if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
     if ((rc = ensure(h->draw, F * px * 2))) return rc;
@@ -242,9 +244,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
 
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[0], st));
-    int16_t* C = (int16_t*)h->C.p;
+    h->path_slack = slack;
+    int16_t* C = (int16_t*)h->C.p + slack;
     int16_t* Caux = (int16_t*)h->Caux.p;
-    int16_t* Lr = (int16_t*)h->Lr.p;  // [P][F][H][W1][D]
+    int16_t* Lr = (int16_t*)h->Lr.p + slack;  // [P-1][F][H][W1][D]
     int16_t* draw = (int16_t*)h->draw.p;
     int16_t* dlr = (int16_t*)h->dlr.p;
 
@@ -785,12 +788,13 @@ int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int*
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) {
     if (!h || !dst) return fail(SDR_ERR_ARG, "null argument");
     const Buf* b = stage == 0 ? &h->C : stage == 1 ? &h->draw : stage == 2 ? &h->dlr
-                 : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : nullptr;
+                 : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : stage == 5 ? &h->keys2 : nullptr;
     if (!b) return fail(SDR_ERR_ARG, "bad stage");
-    if (!b->p || bytes > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
+    const size_t skip = (stage == 0 || stage == 4) ? h->path_slack * 2 : 0;  // front slack
+    if (!b->p || bytes + skip > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));
     SDR_HIP(hipStreamSynchronize(h->stream));
-    SDR_HIP(hipMemcpy(dst, b->p, bytes, hipMemcpyDeviceToHost));
+    SDR_HIP(hipMemcpy(dst, (const char*)b->p + skip, bytes, hipMemcpyDeviceToHost));
     return SDR_OK;
 }
 

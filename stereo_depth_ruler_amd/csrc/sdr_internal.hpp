@@ -56,6 +56,7 @@ struct CostArgs {
     int TY;                  // tile height (output rows)
 };
 
+
 // ---- path aggregation (sdr_paths.hip) ----
 constexpr int kMaxPathDirs = 24;
 constexpr int kMaxPaths = 8;
@@ -81,9 +82,10 @@ struct PathLaunch {
 // top-to-bottom direction fused with the WTA (sdr_paths.hip): the other P-1 directions' L in
 // sum order with the fused direction at position kSouthIdx
 constexpr int kSouthIdx = 2;  // summation order E, W, S, SE, SW, N, NE, NW
-// rows of slack after the cost volume and after the last path buffer: k_south_wta's loads run
-// up to this many rows past a chain's end instead of being clamped
-constexpr int kSouthPad = 48;
+// rows of slack before and after the cost volume and the path-cost buffers: the path kernels'
+// prefetch runs up to this many rows (or pixels) past either end of a chain instead of being
+// clamped
+constexpr int kSouthPad = 64;
 struct SouthWtaArgs {
     const int16_t* L[kMaxPaths];  // the P-1 other directions, in order, S removed
     int npaths;

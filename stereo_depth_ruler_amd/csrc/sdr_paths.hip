@@ -124,6 +124,7 @@ struct Chain {
     int x0, y0, dx, dy, len, kwrite;
 };
 
+
 __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d, int c) {
     Chain ch;
     const int W1 = g.W1, H = g.H;
@@ -188,10 +189,18 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
     return L;
 }
 
+#ifndef SDR_PATHS_LA
+#define SDR_PATHS_LA 16  // k_paths lookahead (steps)
+#endif
 template <int DPL, bool PAD, bool NT = false>
 __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     constexpr int K = DPL / 2;
-    constexpr int PF = 16;
+    // C is loaded LA steps ahead into a ring of 2*LA slots: the slot a load fills was consumed
+    // LA steps earlier, so every slot keeps one register across the loop's back edge (a ring
+    // of LA slots makes the compiler copy the in-flight loads at the back edge, which waits for
+    // all of them)
+    constexpr int LA = SDR_PATHS_LA;
+    constexpr int R = 2 * LA;
     const int lane = threadIdx.x & 63;
     // wave-uniform chain index in an SGPR: all chain control flow stays scalar
     const int cg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -205,26 +214,27 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
 
     const int D = g.D, W1 = g.W1;
     const bool active = !PAD || lane * DPL < D;
-    // addresses = wave-uniform base (SGPRs, scalar arithmetic) + 32-bit lane byte offset;
-    // inactive (padding) lanes read the pixel's last word and discard it
+    // addresses = wave-uniform row base (SGPRs, two scalar adds per step) + 32-bit lane byte
+    // offset; inactive (padding) lanes read the pixel's last word and discard it.  Loads run LA
+    // steps past either end of a chain into the buffers' slack (kSouthPad rows each side), so
+    // neither the addresses nor the stores need a clamp or a branch.
     const uint32_t lofs = (uint32_t)((PAD ? min(lane, D / DPL - 1) : lane) * DPL * 2);
     const ptrdiff_t rowb = (ptrdiff_t)(ch.dy * W1 + ch.dx) * D * 2;
     const size_t p0 = (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D;
-    const char* cbase = (const char*)(pl.C + p0);
-    char* obase = (char*)(pd.out + p0);
-    // 3WAY stripes: a DIR_S chain starting at aux_row0 reads stripe-local cost rows first
-    const int naux = pd.Caux ? pd.aux_rows : 0;
-    const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D) : cbase;
+    const char* cp = (const char*)(pl.C + p0);  // row k + LA's pixel
+    char* op = (char*)(pd.out + p0);            // row k's pixel
     const int last = ch.len - 1;
-    auto cload = [&](int k) __attribute__((always_inline)) {
-        const char* base = (k < naux ? abase : cbase) + (ptrdiff_t)k * rowb;
+    auto cload = [&](const char* base) __attribute__((always_inline)) {
         if constexpr (SDR_PATHS_BUF) return load_buf<K>(rsrc_at(base), lofs);
         else return load_regs<K>((const int16_t*)(base + lofs));
     };
 
-    Regs<K> cring[PF];
+    Regs<K> cring[R];
 #pragma unroll
-    for (int j = 0; j < PF; j++) cring[j] = cload(min(j, last));
+    for (int j = 0; j < LA; j++) {
+        cring[j] = cload(cp);
+        cp += rowb;
+    }
 
     Regs<K> Lp;
 #pragma unroll
@@ -232,20 +242,22 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
     uint32_t delta2 = P2x2;  // minLp + P2 with minLp = 0 before the first pixel
 
-    auto step = [&](const int k, auto jc) __attribute__((always_inline)) {
+    auto step = [&](const int, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const Regs<K> c = cring[j];
-        cring[j] = cload(min(k + PF, last));
+        cring[(j + LA) % R] = cload(cp);
+        cp += rowb;
         const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
-        if (k >= ch.kwrite && active) {
-            if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(obase + (ptrdiff_t)k * rowb), lofs, L);
-            else if constexpr (NT) store_regs_nt<K>((int16_t*)(obase + (ptrdiff_t)k * rowb + lofs), L);
-            else store_regs<K>((int16_t*)(obase + (ptrdiff_t)k * rowb + lofs), L);
+        if (active) {  // padding lanes alias the pixel's last word
+            if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(op), lofs, L);
+            else if constexpr (NT) store_regs_nt<K>((int16_t*)(op + lofs), L);
+            else store_regs<K>((int16_t*)(op + lofs), L);
         }
+        op += rowb;
     };
     int k0 = 0;
-    for (; k0 + PF <= ch.len; k0 += PF) unroll_rows(step, k0, std::make_integer_sequence<int, PF>{});
-    unroll_rows_tail(step, k0, last, std::make_integer_sequence<int, PF - 1>{});
+    for (; k0 + R <= ch.len; k0 += R) unroll_rows(step, k0, std::make_integer_sequence<int, R>{});
+    unroll_rows_tail(step, k0, last, std::make_integer_sequence<int, R - 1>{});
 }
 
 // Path-cost stores are non-temporal (nt): measured on MI355X (C2, 2 frames in flight) +4 % fps
@@ -267,12 +279,12 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 // The top-to-bottom direction fused with A.8 (WTA / uniqueness / subpixel / disp2 scatter).
 //
 // One workgroup per column chain, two roles:
-//   wave 0 (producer) runs the serial recurrence of the chain (C prefetched kSouthPFP rows
-//     ahead) and stages each row's L in LDS, kSouthRB rows per block, two blocks double-buffered;
+//   wave 0 (producer) runs the serial recurrence of the chain (C loaded kSouthLAB blocks
+//     ahead) and stages each row's L in LDS, kSouthRB rows per block, double-buffered;
 //   waves 1..3 (consumers) each own 4 rows of a block: a pixel's D disparities sit on one 16-lane
 //     DPP row (4 pixels per wave instruction, 16 B per lane per direction), the other P-1
-//     directions' L are read from HBM (prefetched whole blocks ahead), the staged L is added from
-//     LDS, and the winner-take-all runs on the saturated sums.
+//     directions' L are read from HBM (prefetched whole blocks ahead), the staged L is added
+//     from LDS, and the winner-take-all runs on the saturated sums.
 // A block is handed over by one barrier.  The serial chain is the only latency-bound part and
 // it does nothing but the recurrence; the WTA and the HBM reads of the other directions run on
 // three more waves beside it.  L of this direction is never written to HBM, so the pass moves
@@ -286,21 +298,60 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 // the 1152 column chains of a 1280x720 d=128 frame are resident in one pass
 constexpr int kSouthConsumers = 3;
 constexpr int kSouthRB = 4 * kSouthConsumers;  // rows per block (4 per consumer wave)
-constexpr int kSouthPFP = 2 * kSouthRB;        // producer prefetch distance in rows (two blocks)
+#ifndef SDR_SOUTH_LAB
+#define SDR_SOUTH_LAB 1
+#endif
+constexpr int kSouthLAB = SDR_SOUTH_LAB;  // producer lookahead in blocks (D <= 128; 1 above)
+#ifndef SDR_SOUTH_PD
+#define SDR_SOUTH_PD 0  // consumer prefetch distance in blocks; 0: by register budget
+#endif
+
+#ifndef SDR_SOUTH_STAMP
+#define SDR_SOUTH_STAMP 0  // diagnostic build: per-wave cycles (total, in barriers) into keys2
+#endif
+// barrier with optional wait-time accounting (SDR_SOUTH_STAMP)
+struct StampBarrier {
+    uint64_t t0 = 0, wait = 0;
+    __device__ __forceinline__ void start() {
+        if constexpr (SDR_SOUTH_STAMP) t0 = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void sync() {
+        if constexpr (SDR_SOUTH_STAMP) {
+            const uint64_t a = __builtin_amdgcn_s_memtime();
+            __syncthreads();
+            wait += __builtin_amdgcn_s_memtime() - a;
+        } else {
+            __syncthreads();
+        }
+    }
+    __device__ __forceinline__ void finish(uint32_t* keys, int slot, int lane) {
+        if constexpr (SDR_SOUTH_STAMP) {
+            const uint64_t tot = __builtin_amdgcn_s_memtime() - t0;
+            if (lane == 0) {
+                ((uint64_t*)keys)[2 * slot] = tot;
+                ((uint64_t*)keys)[2 * slot + 1] = wait;
+            }
+        }
+    }
+};
 
 template <int DPL, bool PAD, int NP>
 __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g, PathLaunch pl,
                                                                            SouthWtaArgs a) {
     constexpr int K = DPL / 2;
-    constexpr int RB = kSouthRB, PFP = kSouthPFP;
-    static_assert(PFP == 2 * RB, "the producer ring spans two row blocks");
-    static_assert(PFP + RB <= kSouthPad, "prefetch overrun must fit the buffers' row slack");
+    constexpr int RB = kSouthRB;
+    constexpr int LAB = K == 1 ? kSouthLAB : 1;  // producer lookahead in blocks
+    constexpr int LA = LAB * RB;                 // ... in rows
+    constexpr int NS = 2 * LAB;                  // ring blocks per producer loop body
+    constexpr int R = NS * RB;                   // producer ring slots (rows)
+    static_assert(LA + RB <= kSouthPad, "load overrun must fit the buffers' row slack");
     constexpr int WDPL = DPL * 4;  // consumer: disparities per lane
     constexpr int WK = WDPL / 2;
     constexpr int DMAX = 64 * DPL;
     constexpr int LSTR = DMAX / 2 + 4;  // dwords per staged row (padded: rows of a wave's 4 pixels)
-    // consumer prefetch distance in blocks: the ring of the other directions' L within ~32 VGPRs
-    constexpr int PD = NP * WK <= 8 ? 3 : (NP * WK <= 16 ? 2 : 1);
+    // consumer prefetch distance in blocks: the ring (2*PD blocks) of the other directions' L
+    constexpr int PD = SDR_SOUTH_PD ? SDR_SOUTH_PD : (NP * WK <= 8 ? 2 : 1);
+    static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
     __shared__ uint32_t sL[2][RB][LSTR];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -312,59 +363,61 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     const Chain ch = make_chain(g, pd, cg - pl.prefix[di]);
     if (ch.len <= 0) return;  // whole workgroup
     const int D = g.D, W1 = g.W1;
-    const ptrdiff_t pstep = (ptrdiff_t)W1 * D;
-    const size_t p0 = (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D;
+    const size_t fofs = (size_t)f * pl.cs_fstride;
     const int last = ch.len - 1;
     const int nblk = (ch.len + RB - 1) / RB;
+    StampBarrier sb;
+    sb.start();
+    const int stamp_slot = (blockIdx.y * gridDim.x + blockIdx.x) * (1 + kSouthConsumers) + wv;
 
     if (wv == 0) {
         // ---------------- producer: the recurrence, L rows to LDS ----------------
         __builtin_amdgcn_s_setprio(2);
         const bool active = !PAD || lane * DPL < D;
-        // addresses = wave-uniform row base (SGPRs, scalar arithmetic) + 32-bit lane byte offset
         const uint32_t lofs = (uint32_t)((PAD ? min(lane, D / DPL - 1) : lane) * DPL * 2);
-        const char* cbase = (const char*)(pl.C + p0);
-        // 3WAY stripes: a chain starting at aux_row0 reads stripe-local cost rows first
+        const ptrdiff_t rowb = (ptrdiff_t)W1 * D * 2;
+        // 3WAY stripes: a chain starting at aux_row0 reads its first aux_rows (< LA) cost rows
+        // from the stripe-local (row-major) buffer; every later row comes from C
         const int naux = pd.Caux ? pd.aux_rows : 0;
-        const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D) : cbase;
-        const ptrdiff_t rowb = pstep * 2;
-        auto cload = [&](int k) __attribute__((always_inline)) {
-            const char* base = (k < naux ? abase : cbase) + (ptrdiff_t)k * rowb;
+        const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D)
+                                    : (const char*)pl.C;
+        const char* cp = (const char*)(pl.C + fofs + ((size_t)ch.y0 * W1 + ch.x0) * D);  // row k + LA
+        auto cload = [&](const char* base) __attribute__((always_inline)) {
             if constexpr (SDR_SOUTH_BUF) return load_buf<K>(rsrc_at(base), lofs);
             else return load_regs<K>((const int16_t*)(base + lofs));
         };
-        Regs<K> cring[PFP];
+        // ring of 2*LA rows loaded LA ahead (see k_paths: no copies at the loop's back edge)
+        Regs<K> cring[R];
 #pragma unroll
-        for (int j = 0; j < PFP; j++) cring[j] = cload(j);
+        for (int j = 0; j < LA; j++) {
+            cring[j] = cload(j < naux ? abase + (ptrdiff_t)j * rowb : cp);
+            cp += rowb;
+        }
         Regs<K> Lp;
 #pragma unroll
         for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
         const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
         uint32_t delta2 = P2x2;
-        // ring slot j = k % PFP; LDS slot = block parity = j / RB
-        auto step = [&](const int k, auto jc) __attribute__((always_inline)) {
-            constexpr int j = decltype(jc)::value;
-            const Regs<K> c = cring[j];
-            cring[j] = cload(k + PFP);
-            const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
+        // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
+        auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
+            uint32_t* dst = &sL[bb & 1][0][lane * K];
+            auto st = [&](const int, auto jc) __attribute__((always_inline)) {
+                constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
+                const Regs<K> c = cring[j];
+                cring[(j + LA) % R] = cload(cp);
+                cp += rowb;
+                const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
 #pragma unroll
-            for (int i = 0; i < K; i++) sL[j / RB][j % RB][lane * K + i] = L.r[i];
-        };
-        auto step_hi = [&](const int k, auto jc) __attribute__((always_inline)) {
-            step(k, std::integral_constant<int, decltype(jc)::value + RB>{});
+                for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];
+            };
+            unroll_rows(st, bb * RB, std::make_integer_sequence<int, RB>{});
+            sb.sync();
         };
         int b = 0;
-        for (; b + 2 <= nblk; b += 2) {
-            unroll_rows(step, b * RB, std::make_integer_sequence<int, RB>{});
-            __syncthreads();
-            unroll_rows(step_hi, b * RB + RB, std::make_integer_sequence<int, RB>{});
-            __syncthreads();
-        }
-        if (b < nblk) {
-            unroll_rows(step, b * RB, std::make_integer_sequence<int, RB>{});
-            __syncthreads();
-        }
-        __syncthreads();  // the consumers' last block
+        for (; b + NS <= nblk; b += NS) unroll_rows(block, b, std::make_integer_sequence<int, NS>{});
+        unroll_rows_tail(block, b, nblk - 1, std::make_integer_sequence<int, NS - 1>{});
+        sb.sync();  // the consumers' last block
+        sb.finish(a.keys2, stamp_slot, lane);
         return;
     }
 
@@ -373,9 +426,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     const int r = (wv - 1) * 4 + grp;  // this lane group's row within a block
     const bool wactive = !PAD || gl * WDPL < D;
     const int wd0 = (PAD ? min(gl, D / WDPL - 1) : gl) * WDPL;
-    // addresses = wave-uniform block base (SGPRs) + 32-bit lane byte offset (row r, disparity wd0)
-    const ptrdiff_t bstepb = (ptrdiff_t)RB * pstep * 2;
-    const uint32_t lofs = (uint32_t)(((size_t)r * pstep + wd0) * 2);
+    // row blk*RB + r of the chain: wave-uniform block base + lane byte offset
+    const ptrdiff_t bstepb = (ptrdiff_t)RB * W1 * D * 2;
+    const uint32_t lofs = (uint32_t)(((size_t)r * W1 * D + wd0) * 2);
+    const size_t p0 = fofs + ((size_t)ch.y0 * W1 + ch.x0) * D;
     auto oload = [&](int q, int blk) __attribute__((always_inline)) {
         const char* base = (const char*)(a.L[q] + p0) + (ptrdiff_t)blk * bstepb;
         if constexpr (SDR_SOUTH_BUF) return load_buf<WK>(rsrc_at(base), lofs);
@@ -392,24 +446,22 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     int16_t* raw = a.disp_raw + (size_t)f * a.disp_fstride + x + g.minX1;
     uint32_t* keys = a.keys2 + (size_t)f * a.disp_fstride;
 
-    Regs<WK> oring[PD][NP];
+    // ring of 2*PD blocks loaded PD ahead (as the producer's: no copies at the back edge);
+    // unconditional: blocks past the chain's end read the buffers' row slack (kSouthPad)
+    constexpr int OR = 2 * PD;
+    Regs<WK> oring[OR][NP];
 #pragma unroll
-    for (int s = 0; s < PD; s++) {
-        if (s < nblk) {
+    for (int s = 0; s < PD; s++)
 #pragma unroll
-            for (int q = 0; q < NP; q++) oring[s][q] = oload(q, s);
-        }
-    }
+        for (int q = 0; q < NP; q++) oring[s][q] = oload(q, s);
 
-    auto consume = [&](const int b, auto sc) __attribute__((always_inline)) {
+    auto consume_sync = [&](const int b, auto sc) __attribute__((always_inline)) {
         constexpr int s = decltype(sc)::value;
         Regs<WK> o[NP];
 #pragma unroll
         for (int q = 0; q < NP; q++) o[q] = oring[s][q];
-        if (b + PD < nblk) {
 #pragma unroll
-            for (int q = 0; q < NP; q++) oring[s][q] = oload(q, b + PD);
-        }
+        for (int q = 0; q < NP; q++) oring[(s + PD) % OR][q] = oload(q, b + PD);
         // S = sat(sum of the P path costs), the fused direction's L from LDS
         const uint32_t* ls = &sL[b & 1][r][wd0 / 2];
         Regs<WK> St;
@@ -477,15 +529,13 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             }
             raw[y * g.W] = (int16_t)out;
         }
+        sb.sync();
     };
-    auto consume_sync = [&](const int b, auto sc) __attribute__((always_inline)) {
-        consume(b, sc);
-        __syncthreads();
-    };
-    __syncthreads();  // block 0 staged
+    sb.sync();  // block 0 staged
     int b = 0;
-    for (; b + PD <= nblk; b += PD) unroll_rows(consume_sync, b, std::make_integer_sequence<int, PD>{});
-    unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, PD - 1>{});
+    for (; b + OR <= nblk; b += OR) unroll_rows(consume_sync, b, std::make_integer_sequence<int, OR>{});
+    unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, OR - 1>{});
+    sb.finish(a.keys2, stamp_slot, lane);
 }
 
 // disp_raw := invalid, keys2 := no match (per frame, before k_south_wta)

@@ -188,10 +188,15 @@ class StereoSGBM:
         return disp, xyz
 
     def debug_stage(self, stage: int, shape, dtype):
-        """Copy an internal buffer of the last compute (0 C, 1 raw WTA, 2 LR, 3 final, 4 path costs)."""
+        """Copy an internal buffer of the last compute (0 C, 1 raw WTA, 2 LR, 3 final, 4 path costs,
+        5 disp2 keys)."""
         out = np.empty(shape, dtype)
         check(lib().sdr_sgbm_debug_stage(self._h, int(stage), out.ctypes.data, out.nbytes))
         return out
+
+    def debug_cost_volume(self, H: int, W1: int, D: int) -> np.ndarray:
+        """The first frame's cost volume C of the last compute as (H, W1, D) int16."""
+        return self.debug_stage(0, (H, W1, D), np.int16)
 
     def enable_timing(self, level=1):
         """0 off, 1 per-stage events, 2 per-stage + per-kernel-launch events."""

@@ -98,7 +98,7 @@ def test_cost_volume_bit_exact(oracle):
         args = (0, 48, 5, 600, 2400, 1, 63, 12, 0, 0, mode)
         m = sdr.StereoSGBM.create(*args)
         m.compute(L, R)
-        C = m.debug_stage(0, (40, 150 - 48, 48), np.int16)
+        C = m.debug_cost_volume(40, 150 - 48, 48)
         assert np.array_equal(C, oracle.cost_volume(L, R, oracle.make_params(*args)))
 
 

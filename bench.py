@@ -172,7 +172,8 @@ def main():
     from stereo_depth_ruler_amd.distributed import as_bytes
     from stereo_depth_ruler_amd import sgbm as _sg
     KERNEL_KINDS = {"prefilter": _sg.KERNEL_PREFILTER, "k_cost": _sg.KERNEL_COST, "k_paths": _sg.KERNEL_PATHS,
-                    "k_wta_lr": _sg.KERNEL_WTA_LR, "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
+                    "k_south_wta": _sg.KERNEL_WTA_LR, "k_lr_check": _sg.KERNEL_LR_CHECK,
+                    "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
                     "reproject": _sg.KERNEL_REPROJECT}
 
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
@@ -288,20 +289,22 @@ def main():
         frames_seen = per_kind["prefilter"][1]
         if not cnt:
             return kern, None
-        # k_paths: every direction reads C (2 B/cell) and writes its own L_r (2 B/cell)
-        bytes_per_launch = cells * 4 * P
+        # k_paths runs every direction except top-to-bottom (that one is fused into k_south_wta):
+        # each of its P-1 directions reads C (2 B/cell) and writes its own L_r (2 B/cell)
+        bytes_per_launch = cells * 4 * (P - 1)
         avg_s = tot_ms / cnt / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
         roof = {
             "bound": "hbm",
-            "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> (all {P} path directions of a batch in one launch)",
+            "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> ({P - 1} of the {P} path directions of a batch "
+                      f"in one launch; the top-to-bottom one is fused into k_south_wta)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": load_traffic(f"{a.config}:k_paths"),
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "bytes_model": f"4*P*cells, P={P}, cells=batch*H*W1*D={cells}",
+            "bytes_model": f"4*(P-1)*cells, P={P}, cells=batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),
             "launches_timed": cnt,
             "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
@@ -321,14 +324,16 @@ def main():
     roofline = None
     kernels = None
     if not a.no_kernel_timing:
-        kernels, roofline = kernel_report(m)
-        if roofline is not None:
-            roofline["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
-                                    f"({ns} frames in flight: launches share the GPU with the other "
-                                    f"streams' kernels)")
-        if ns > 1 and roofline is not None:
-            # the same kernels with nothing beside them: a short single-stream segment after the
-            # timed region (kernel quality; the timed region's numbers include the overlap)
+        kernels, inflight = kernel_report(m)
+        roofline = inflight
+        if inflight is not None:
+            inflight["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
+                                    f"({ns} frames in flight: an event pair also spans the wait for CUs "
+                                    f"held by the other streams' kernels, so it overstates the duration)")
+        if ns > 1 and inflight is not None:
+            # the dominant kernel's roofline: the same launches with nothing beside them, a
+            # single-stream segment timed right after the timed region (rocprofv3's per-dispatch
+            # durations of these launches agree: profiles/r1_segments_c2.md)
             torch.cuda.synchronize()
             m.kernel_time(-1, reset=True)
             with torch.cuda.stream(streams[0]):
@@ -336,14 +341,22 @@ def main():
                     j = (i * batch) % (nf - batch + 1) if nf > batch else 0
                     run(j, 0, 0)
             torch.cuda.synchronize()
-            iso_k, iso_r = kernel_report(m)
-            iso_r["measured"] = f"HIP events, {a.iso_steps} single-stream steps after the timed region"
-            iso_r["kernels"] = iso_k
-            roofline["isolated"] = iso_r
+            iso_k, roofline = kernel_report(m)
+            roofline["measured"] = (f"HIP events around each launch, {a.iso_steps} single-stream steps "
+                                    f"after the timed region")
+            roofline["kernels"] = iso_k
+            roofline["in_flight"] = inflight
         m.enable_timing(0)
-
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6
+    if roofline is not None:
+        # B_frame = cells*(2+6P) + 16 B/px, times the whole job's frame rate
+        b_frame = cells * (2 + 6 * P) + 16 * Hm * Wm * batch
+        job = b_frame * world * a.steps / el / 1e9
+        roofline["job"] = {"model_bytes_per_step": b_frame, "achieved": round(job, 1),
+                           "frac": round(job / HBM_PEAK_GBS / world, 4),
+                           "note": "canonical unfused data-flow bytes x steps/s (per GPU); the fused "
+                                   "kernels move fewer real bytes"}
     out = {
         "metric": METRIC,
         "value": round(value, 3),

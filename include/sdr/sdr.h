@@ -270,8 +270,10 @@ size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, i
  * brackets every kernel launch; sdr_sgbm_kernel_time sums the launches of one SDR_KERNEL_* kind
  * (kind < 0: all) since the last reset. */
 enum {
-    SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATHS = 2, SDR_KERNEL_WTA_LR = 3,
-    SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6
+    SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATHS = 2,
+    SDR_KERNEL_WTA_LR = 3,   /* k_south_wta: top-to-bottom path fused with WTA/uniqueness/disp2 */
+    SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6,
+    SDR_KERNEL_LR_CHECK = 7  /* k_lr_check */
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);

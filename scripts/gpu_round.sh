@@ -17,5 +17,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
   python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline > "$O/prof.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_s1" -o run -- \
   python3 bench.py --steps 60 --warmup 10 --no-cpu-baseline --streams 1 > "$O/prof_s1.log" 2>&1
+python3 scripts/trace_segments.py "$O/prof" --iso 30 --out "$O/segments.md" > /dev/null
 echo prof-done
 timeout -k 10 900 bash scripts/pmc_profile.sh "$O/pmc"

@@ -350,7 +350,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     wa.uniq = e.uniq;
     wa.uniq_simd = e.uniq_simd;
     { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
-    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st); }
+    { KTimer kt(h, SDR_KERNEL_LR_CHECK); sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st); }
     const bool speckle = e.speckle_ws > 0;
     { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, speckle ? dfin : dst, W, H, F, st); }
     if (speckle) {

@@ -142,6 +142,9 @@ struct sdr_sgbm {
     std::vector<int> kkind;
     size_t kused = 0;
     size_t path_slack = 0;  // elements of slack in front of C and Lr (last compute)
+    // class path: the right matcher runs on a side stream forked from / joined to this one
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -434,6 +437,10 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     for (auto ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto ev : h->kev) (void)hipEventDestroy(ev);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->fork) (void)hipEventDestroy(h->fork);
+    if (h->join) (void)hipEventDestroy(h->join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
     return SDR_OK;
@@ -693,17 +700,28 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
     int16_t* dl = (int16_t*)left->cls_dl.p;
     int16_t* dr = (int16_t*)left->cls_dr.p;
     int16_t* dw = d_filtered ? d_filtered : (int16_t*)left->cls_wls.p;
-    // matcher->compute(L, R) (stereo_disparity.cpp:27)
+    // right_matcher->compute(R, L) (stereo_disparity.cpp:28) and matcher->compute(L, R) (:27) are
+    // independent until the WLS filter: the right one runs on a side stream forked from the
+    // caller's and joined back before the filter (at 640x360 each matcher's row chains fill
+    // under a third of the chip, so the two overlap)
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
     if (right) {
-        // right_matcher->compute(R, L) (stereo_disparity.cpp:28), same stream
+        if (!left->side) {
+            SDR_HIP(hipStreamCreateWithFlags(&left->side, hipStreamNonBlocking));
+            SDR_HIP(hipEventCreateWithFlags(&left->fork, hipEventDisableTiming));
+            SDR_HIP(hipEventCreateWithFlags(&left->join, hipEventDisableTiming));
+        }
+        SDR_HIP(hipEventRecord(left->fork, st));
+        SDR_HIP(hipStreamWaitEvent(left->side, left->fork, 0));
         hipStream_t rs = right->stream;
-        right->stream = st;
+        right->stream = left->side;
         rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
         right->stream = rs;
         if (rc) return rc;
+        SDR_HIP(hipEventRecord(left->join, left->side));
     }
+    if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
+    if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
     const int16_t* res = dl;
     if (wls) {
         // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)

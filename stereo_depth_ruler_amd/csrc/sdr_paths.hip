@@ -157,11 +157,58 @@ __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d,
     return ch;
 }
 
+#ifndef SDR_PATHS_VF
+// offset-carrying recurrence (1) or the normalised form (0).  Both are bit-exact on MI355X; the
+// shorter serial chain did not pay (C2 single-stream k_paths 322 us with 1, 304-315 us with 0,
+// k_south_wta within noise): a step's time is not set by this dependency chain.
+#define SDR_PATHS_VF 0
+#endif
+// Initial recurrence state before a chain's first pixel (Lp = 0 there, OpenCV's zeroed row).
+__device__ __forceinline__ uint32_t path_delta0(uint32_t P2x2) { return SDR_PATHS_VF ? 0u : P2x2; }
+
 // One step of the path recurrence on a wave's packed int16 pairs (lane l: disparities
-// [l*2K, l*2K + 2K)); Lp := L, delta2 := minL + P2 (both halves).
+// [l*2K, l*2K + 2K)); returns L of this pixel.
+//
+// SDR_PATHS_VF=1 carries V(k) = L(k) + delta(k) instead of L(k) (delta(k) = min_d L(k-1) + P2):
+//   V(k+1) = C - delta(k) + min(min(V[d], V[d-1] + P1, V[d+1] + P1), M(k) + P2),
+//   delta(k+1) = M(k) - delta(k) + P2,  M(k) = min_d V(k),  L(k) = V(k) - delta(k),
+// which is the same integer arithmetic (0 <= L <= V <= 2 Cmax + P2, the range the normalised form
+// already needs for C + min(...)), but the wave-wide minimum of a step is taken over the state it
+// starts from, so it runs beside the neighbour terms instead of after them: the serial chain from
+// one pixel to the next is the reduction plus three ops.  State: Lp = V, delta2 = delta.
+// SDR_PATHS_VF=0: Lp := L, delta2 := minL + P2 (both halves).
 template <int K, bool PAD>
 __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
                                              uint32_t P2x2, bool active) {
+    if constexpr (SDR_PATHS_VF) {
+        uint32_t m = Lp.r[0];
+#pragma unroll
+        for (int i = 1; i < K; i++) m = pk_min(m, Lp.r[i]);
+        m = pk_min(m, funnel16(m, m));
+        m = wave_min_u32(m);  // M(k) in both halves
+        const uint32_t up = lane_from_prev(Lp.r[K - 1], kMaxPair);
+        const uint32_t dn = lane_from_next(Lp.r[0], kMaxPair);
+        const uint32_t mP2 = pk_add(m, P2x2);
+        const uint32_t dnew = pk_sub(mP2, delta2);
+        Regs<K> V, L;
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
+            const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
+            const uint32_t t = pk_min(pk_add_sat(pk_min(dm1, dp1), P1x2), Lp.r[i]);
+            uint32_t v = pk_add(pk_min(t, mP2), pk_sub(c.r[i], delta2));
+            uint32_t l = pk_sub(v, dnew);
+            if constexpr (PAD) {
+                v = active ? v : kMaxPair;
+                l = active ? l : kMaxPair;
+            }
+            V.r[i] = v;
+            L.r[i] = l;
+        }
+        Lp = V;
+        delta2 = dnew;
+        return L;
+    }
     if constexpr (PAD) {
 #pragma unroll
         for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
@@ -240,7 +287,7 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
 #pragma unroll
     for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
     const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
-    uint32_t delta2 = P2x2;  // minLp + P2 with minLp = 0 before the first pixel
+    uint32_t delta2 = path_delta0(P2x2);  // before the first pixel (see path_step)
 
     auto step = [&](const int, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
@@ -397,7 +444,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
 #pragma unroll
         for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
         const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
-        uint32_t delta2 = P2x2;
+        uint32_t delta2 = path_delta0(P2x2);
         // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
         auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
             uint32_t* dst = &sL[bb & 1][0][lane * K];

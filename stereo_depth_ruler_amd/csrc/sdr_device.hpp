@@ -115,6 +115,22 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t m) {
     return min((uint32_t)p32[0], (uint32_t)p32[1]);
 }
 
+// The same minimum as a wave-uniform value: row minima by DPP, then the GFX9 row broadcasts
+// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3) leave the wave's minimum in
+// lane 63, read into an SGPR.  Four fewer VALU ops than the permlane-swap tail, and the result
+// feeds the next ops as a scalar operand.
+__device__ __forceinline__ uint32_t wave_min_u32_uniform(uint32_t m) {
+    m = min_u32_dpp<kDppQuadXor1>(m);
+    m = min_u32_dpp<kDppQuadXor2>(m);
+    m = min_u32_dpp<kDppRowHalfMirror>(m);
+    m = min_u32_dpp<kDppRowMirror>(m);
+    uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m, 0x142, 0xa, 0xf, false);
+    m = min(m, t);
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m, 0x143, 0xc, 0xf, false);
+    m = min(m, t);
+    return (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+}
+
 // Unsigned 32-bit minimum over each 16-lane DPP row, broadcast within the row.
 __device__ __forceinline__ uint32_t row16_min_u32(uint32_t m) {
     m = min_u32_dpp<kDppQuadXor1>(m);

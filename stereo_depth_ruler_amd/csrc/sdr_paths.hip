@@ -74,6 +74,12 @@ __device__ __forceinline__ void store_regs(int16_t* p, const Regs<K>& v) {
 #ifndef SDR_PATHS_BUF
 #define SDR_PATHS_BUF 1  // k_paths through buffer resources (0: flat global addresses)
 #endif
+#ifndef SDR_WMIN_BCAST
+#define SDR_WMIN_BCAST 1  // path minimum via DPP row broadcasts + readlane (0: permlane swaps)
+#endif
+#ifndef SDR_PATHS_SOFF
+#define SDR_PATHS_SOFF 1  // k_paths: per-chain resources + SGPR offsets (0: a resource per access)
+#endif
 #ifndef SDR_SOUTH_BUF
 #define SDR_SOUTH_BUF 1  // k_south_wta through buffer resources (0: flat global addresses)
 #endif
@@ -100,6 +106,44 @@ __device__ __forceinline__ Regs<K> load_buf(Rsrc r, uint32_t vofs) {
         }
     }
     return v;
+}
+
+// The same with a wave-uniform (SGPR) byte offset: one resource per buffer for a whole chain,
+// and one scalar add per step moves every access of the step.
+template <int K>
+__device__ __forceinline__ Regs<K> load_buf_so(Rsrc r, uint32_t vofs, uint32_t sofs) {
+    Regs<K> v;
+    if constexpr (K == 1) {
+        v.r[0] = __builtin_amdgcn_raw_buffer_load_b32(r, vofs, sofs, 0);
+    } else if constexpr (K == 2) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, vofs, sofs, 0);
+        v.r[0] = t[0];
+        v.r[1] = t[1];
+    } else {
+        static_assert(K % 4 == 0, "K = 1, 2 or a multiple of 4");
+#pragma unroll
+        for (int j = 0; j < K / 4; j++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, vofs + 16 * j, sofs, 0);
+            v.r[4 * j] = t[0]; v.r[4 * j + 1] = t[1]; v.r[4 * j + 2] = t[2]; v.r[4 * j + 3] = t[3];
+        }
+    }
+    return v;
+}
+template <int K>
+__device__ __forceinline__ void store_buf_nt_so(Rsrc r, uint32_t vofs, uint32_t sofs, const Regs<K>& v) {
+    if constexpr (K == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(v.r[0], r, vofs, sofs, 2);
+    } else if constexpr (K == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) uint32_t){v.r[0], v.r[1]}, r,
+                                              vofs, sofs, 2);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K / 4; j++)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (__attribute__((ext_vector_type(4))) uint32_t){v.r[4 * j], v.r[4 * j + 1], v.r[4 * j + 2],
+                                                               v.r[4 * j + 3]},
+                r, vofs + 16 * j, sofs, 2);
+    }
 }
 
 // non-temporal (aux = nt) stores of K packed pairs
@@ -230,8 +274,14 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
     }
     // both halves := min of the pair; L >= 0, so the u32 order of such words is the int16 order
     m = pk_min(m, funnel16(m, m));
-    m = wave_min_u32(m);
-    delta2 = pk_add(m, P2x2);
+    if constexpr (SDR_WMIN_BCAST) {
+        // wave-uniform: both halves < 0x8000 and their sums with P2 < 0x10000, so a 32-bit add
+        // of the packed words is the packed add (no carry crosses the halves)
+        delta2 = wave_min_u32_uniform(m) + P2x2;
+    } else {
+        m = wave_min_u32(m);
+        delta2 = pk_add(m, P2x2);
+    }
     Lp = L;
     return L;
 }
@@ -271,8 +321,17 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     const char* cp = (const char*)(pl.C + p0);  // row k + LA's pixel
     char* op = (char*)(pd.out + p0);            // row k's pixel
     const int last = ch.len - 1;
+    // SDR_PATHS_SOFF: one resource per buffer for the whole chain, based at the lowest address
+    // the chain's loads touch (row `low`); the SGPR offset of row j is (j - low) * rowb >= 0, and
+    // the store resource is shifted so that the store of row k uses the offset of the load of
+    // row k + LA, which the step has in hand: one scalar add per step moves both.
+    const int low = rowb >= 0 ? 0 : last + LA;
+    const Rsrc rC = rsrc_at(cp + (ptrdiff_t)low * rowb);
+    const Rsrc rO = rsrc_at(op + (ptrdiff_t)(low - LA) * rowb);
+    uint32_t soff = (uint32_t)((ptrdiff_t)(0 - low) * rowb);
     auto cload = [&](const char* base) __attribute__((always_inline)) {
-        if constexpr (SDR_PATHS_BUF) return load_buf<K>(rsrc_at(base), lofs);
+        if constexpr (SDR_PATHS_SOFF) return load_buf_so<K>(rC, lofs, soff);
+        else if constexpr (SDR_PATHS_BUF) return load_buf<K>(rsrc_at(base), lofs);
         else return load_regs<K>((const int16_t*)(base + lofs));
     };
 
@@ -281,6 +340,7 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     for (int j = 0; j < LA; j++) {
         cring[j] = cload(cp);
         cp += rowb;
+        soff += (uint32_t)rowb;
     }
 
     Regs<K> Lp;
@@ -296,11 +356,13 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
         cp += rowb;
         const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
         if (active) {  // padding lanes alias the pixel's last word
-            if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(op), lofs, L);
+            if constexpr (NT && SDR_PATHS_SOFF) store_buf_nt_so<K>(rO, lofs, soff, L);
+            else if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(op), lofs, L);
             else if constexpr (NT) store_regs_nt<K>((int16_t*)(op + lofs), L);
             else store_regs<K>((int16_t*)(op + lofs), L);
         }
         op += rowb;
+        soff += (uint32_t)rowb;
     };
     int k0 = 0;
     for (; k0 + R <= ch.len; k0 += R) unroll_rows(step, k0, std::make_integer_sequence<int, R>{});

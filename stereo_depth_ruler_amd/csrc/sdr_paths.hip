@@ -74,6 +74,9 @@ __device__ __forceinline__ void store_regs(int16_t* p, const Regs<K>& v) {
 #ifndef SDR_PATHS_BUF
 #define SDR_PATHS_BUF 1  // k_paths through buffer resources (0: flat global addresses)
 #endif
+#ifndef SDR_PATHS_KEEPFILL
+#define SDR_PATHS_KEEPFILL 1  // boundary lanes of the neighbour shifts kept across steps (0: refilled)
+#endif
 #ifndef SDR_WMIN_BCAST
 #define SDR_WMIN_BCAST 1  // path minimum via DPP row broadcasts + readlane (0: permlane swaps)
 #endif
@@ -221,9 +224,12 @@ __device__ __forceinline__ uint32_t path_delta0(uint32_t P2x2) { return SDR_PATH
 // starts from, so it runs beside the neighbour terms instead of after them: the serial chain from
 // one pixel to the next is the reduction plus three ops.  State: Lp = V, delta2 = delta.
 // SDR_PATHS_VF=0: Lp := L, delta2 := minL + P2 (both halves).
+// upr/dnr: the lane-shifted neighbour words of the previous step.  A wave shift leaves the lane
+// without a source (lane 0 / lane 63) unwritten, so passing the previous shift as the DPP's old
+// value keeps the kMaxPair boundary there from the first step on, with no refill per step.
 template <int K, bool PAD>
 __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
-                                             uint32_t P2x2, bool active) {
+                                             uint32_t P2x2, bool active, uint32_t& upr, uint32_t& dnr) {
     if constexpr (SDR_PATHS_VF) {
         uint32_t m = Lp.r[0];
 #pragma unroll
@@ -257,8 +263,14 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
 #pragma unroll
         for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
     }
-    const uint32_t up = lane_from_prev(Lp.r[K - 1], kMaxPair);
-    const uint32_t dn = lane_from_next(Lp.r[0], kMaxPair);
+    uint32_t up, dn;
+    if constexpr (SDR_PATHS_KEEPFILL) {
+        up = upr = lane_from_prev(Lp.r[K - 1], upr);
+        dn = dnr = lane_from_next(Lp.r[0], dnr);
+    } else {
+        up = lane_from_prev(Lp.r[K - 1], kMaxPair);
+        dn = lane_from_next(Lp.r[0], kMaxPair);
+    }
     Regs<K> L;
     uint32_t m = kMaxPair;
 #pragma unroll
@@ -272,13 +284,15 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
         L.r[i] = l;
         m = pk_min(m, l);
     }
-    // both halves := min of the pair; L >= 0, so the u32 order of such words is the int16 order
-    m = pk_min(m, funnel16(m, m));
     if constexpr (SDR_WMIN_BCAST) {
-        // wave-uniform: both halves < 0x8000 and their sums with P2 < 0x10000, so a 32-bit add
-        // of the packed words is the packed add (no carry crosses the halves)
-        delta2 = wave_min_u32_uniform(m) + P2x2;
+        // min of the pair into the low half (one SDWA op; L >= 0, so u16 order is int16 order),
+        // wave minimum as a wave-uniform value, splatted and offset by P2 in scalar registers
+        const uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu),
+                                                                  (unsigned short)(m >> 16));
+        delta2 = wave_min_u32_uniform(m16) * 0x00010001u + P2x2;
     } else {
+        // both halves := min of the pair; L >= 0, so the u32 order of such words is the int16 order
+        m = pk_min(m, funnel16(m, m));
         m = wave_min_u32(m);
         delta2 = pk_add(m, P2x2);
     }
@@ -347,14 +361,15 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
 #pragma unroll
     for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
     const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
-    uint32_t delta2 = path_delta0(P2x2);  // before the first pixel (see path_step)
+    uint32_t delta2 = path_delta0(P2x2);
+    uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
 
     auto step = [&](const int, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const Regs<K> c = cring[j];
         cring[(j + LA) % R] = cload(cp);
         cp += rowb;
-        const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
+        const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
         if (active) {  // padding lanes alias the pixel's last word
             if constexpr (NT && SDR_PATHS_SOFF) store_buf_nt_so<K>(rO, lofs, soff, L);
             else if constexpr (NT && SDR_PATHS_BUF) store_buf_nt<K>(rsrc_at(op), lofs, L);
@@ -507,6 +522,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
         const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
         uint32_t delta2 = path_delta0(P2x2);
+    uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
         // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
         auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
             uint32_t* dst = &sL[bb & 1][0][lane * K];
@@ -515,7 +531,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
                 const Regs<K> c = cring[j];
                 cring[(j + LA) % R] = cload(cp);
                 cp += rowb;
-                const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active);
+                const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
 #pragma unroll
                 for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];
             };

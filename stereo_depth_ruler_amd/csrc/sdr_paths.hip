@@ -206,8 +206,9 @@ __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d,
 
 #ifndef SDR_PATHS_VF
 // offset-carrying recurrence (1) or the normalised form (0).  Both are bit-exact on MI355X; the
-// shorter serial chain did not pay (C2 single-stream k_paths 322 us with 1, 304-315 us with 0,
-// k_south_wta within noise): a step's time is not set by this dependency chain.
+// shorter serial chain did not pay, twice: C2 single-stream k_paths 322 vs 304-315 us before the
+// scalar-minimum rework, 280-282 vs 273-285 us after it, k_south_wta 241-242 us either way (its
+// producer's step time is not set by this dependency chain either).
 #define SDR_PATHS_VF 0
 #endif
 // Initial recurrence state before a chain's first pixel (Lp = 0 there, OpenCV's zeroed row).
@@ -234,12 +235,14 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
         uint32_t m = Lp.r[0];
 #pragma unroll
         for (int i = 1; i < K; i++) m = pk_min(m, Lp.r[i]);
-        m = pk_min(m, funnel16(m, m));
-        m = wave_min_u32(m);  // M(k) in both halves
-        const uint32_t up = lane_from_prev(Lp.r[K - 1], kMaxPair);
-        const uint32_t dn = lane_from_next(Lp.r[0], kMaxPair);
-        const uint32_t mP2 = pk_add(m, P2x2);
-        const uint32_t dnew = pk_sub(mP2, delta2);
+        const uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu),
+                                                                  (unsigned short)(m >> 16));
+        // M(k) + P2 and delta(k+1) as wave-uniform packed words (equal halves, no carry/borrow
+        // crosses them: 0 < delta(k+1) = M(k) + P2 - delta(k) < 0x8000)
+        const uint32_t mP2 = wave_min_u32_uniform(m16) * 0x00010001u + P2x2;
+        const uint32_t dnew = mP2 - delta2;
+        const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
+        const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
         Regs<K> V, L;
 #pragma unroll
         for (int i = 0; i < K; i++) {

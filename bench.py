@@ -231,10 +231,12 @@ def main():
         j = (i * batch) % (nf - batch + 1) if nf > batch else 0
         k = i % ns
         slot = i % (2 * ns)
-        if pending[slot] is not None:
-            pending[slot].wait()
-            pending[slot] = None
         with torch.cuda.stream(streams[k]):
+            # slot s is always issued on stream s % ns: the gather that last read this slot's
+            # buffer must finish before this stream overwrites it (wait() orders the current stream)
+            if pending[slot] is not None:
+                pending[slot].wait()
+                pending[slot] = None
             res = run(j, k, slot)
             if world > 1:
                 # gather this step's disparity from every rank; a later step reuses the slot only

@@ -433,6 +433,9 @@ constexpr int kSouthLAB = SDR_SOUTH_LAB;  // producer lookahead in blocks (D <= 
 #define SDR_SOUTH_PD 0  // consumer prefetch distance in blocks; 0: by register budget
 #endif
 
+#ifndef SDR_SOUTH_LDSU
+#define SDR_SOUTH_LDSU 1  // consumers: S row staged in LDS for subpixel + uniqueness (0: in registers)
+#endif
 #ifndef SDR_SOUTH_STAMP
 #define SDR_SOUTH_STAMP 0  // diagnostic build: per-wave cycles (total, in barriers) into keys2
 #endif
@@ -480,6 +483,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     constexpr int PD = SDR_SOUTH_PD ? SDR_SOUTH_PD : (NP * WK <= 8 ? 2 : 1);
     static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
     __shared__ uint32_t sL[2][RB][LSTR];
+    // SDR_SOUTH_LDSU: each consumer row's S staged in LDS for the subpixel neighbours and the
+    // uniqueness minimum (one 16-B write per lane, three masking u16 writes, one read back)
+    __shared__ uint32_t sS[SDR_SOUTH_LDSU ? kSouthConsumers : 1][4][SDR_SOUTH_LDSU ? DMAX / 2 : 1];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cg = blockIdx.x;
@@ -614,16 +620,37 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             const uint32_t hi = (uint32_t)((int)(short)(St.r[i] >> 16) + 32768);
             key = min(key, min((lo << 16) | d, (hi << 16) | (d + 1)));
         }
+        uint32_t* srow = &sS[SDR_SOUTH_LDSU ? wv - 1 : 0][grp][0];
+        if constexpr (SDR_SOUTH_LDSU) {
+#pragma unroll
+            for (int i = 0; i < WK; i++) ((uint32_t __attribute__((may_alias))*)srow)[gl * WK + i] = St.r[i];
+        }
         key = row16_min_u32(wactive ? key : 0xffffffffu);
         const int minS = (int)(key >> 16) - 32768;
         const int best = (int)(key & 0xffff);
-        // uniqueness: min of S[d] over |d - best| > 1 (0 <= S <= 32767: or-ing 0x7fff masks a half)
+        const int dm = max(best - 1, 0), dp = min(best + 1, D - 1);
+        // uniqueness: min of S[d] over |d - best| > 1 (0 <= S <= 32767: 0x7fff masks a half)
         uint32_t m2 = kMaxPair;
+        int Sm_l = 0, Sp_l = 0;
+        if constexpr (SDR_SOUTH_LDSU) {
+            // the halfword accesses alias the row's 32-bit words: may_alias keeps their order
+            typedef int16_t __attribute__((may_alias)) s16a;
+            typedef uint32_t __attribute__((may_alias)) u32a;
+            s16a* s16 = (s16a*)srow;
+            Sm_l = s16[dm];
+            Sp_l = s16[dp];
+            s16[dm] = 0x7fff;
+            s16[best] = 0x7fff;
+            s16[dp] = 0x7fff;
 #pragma unroll
-        for (int i = 0; i < WK; i++) {
-            const int t = gl * WDPL + 2 * i - best;
-            const uint32_t mk = ((unsigned)(t + 1) <= 2u ? 0x7fffu : 0u) | ((unsigned)(t + 2) <= 2u ? 0x7fff0000u : 0u);
-            m2 = pk_min(m2, St.r[i] | mk);
+            for (int i = 0; i < WK; i++) m2 = pk_min(m2, ((u32a*)srow)[gl * WK + i]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < WK; i++) {
+                const int t = gl * WDPL + 2 * i - best;
+                const uint32_t mk = ((unsigned)(t + 1) <= 2u ? 0x7fffu : 0u) | ((unsigned)(t + 2) <= 2u ? 0x7fff0000u : 0u);
+                m2 = pk_min(m2, St.r[i] | mk);
+            }
         }
         m2 = wactive ? m2 : kMaxPair;
         m2 = pk_min(m2, funnel16(m2, m2));
@@ -633,21 +660,23 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);
         const bool reject = check_uniq && (uniq_simd ? (min2 < thr16) : (min2 * lhs_scale < minS * 100));
         // subpixel: d*16 + ((S[d-1]-S[d+1])*16 + den) / (2*den), C truncating division
-        const int dm = max(best - 1, 0), dp = min(best + 1, D - 1);
-        uint32_t wm = St.r[0], wp = St.r[0];
+        uint32_t am = 0, ap = 0;
+        if constexpr (!SDR_SOUTH_LDSU) {
+            uint32_t wm = St.r[0], wp = St.r[0];
 #pragma unroll
-        for (int i = 1; i < WK; i++) {
-            if (((dm % WDPL) >> 1) == i) wm = St.r[i];
-            if (((dp % WDPL) >> 1) == i) wp = St.r[i];
+            for (int i = 1; i < WK; i++) {
+                if (((dm % WDPL) >> 1) == i) wm = St.r[i];
+                if (((dp % WDPL) >> 1) == i) wp = St.r[i];
+            }
+            am = (uint32_t)__shfl((int)wm, grp * 16 + dm / WDPL);
+            ap = (uint32_t)__shfl((int)wp, grp * 16 + dp / WDPL);
         }
-        const uint32_t am = (uint32_t)__shfl((int)wm, grp * 16 + dm / WDPL);
-        const uint32_t ap = (uint32_t)__shfl((int)wp, grp * 16 + dp / WDPL);
         if (gl == 0 && rowok) {
             const size_t y = (size_t)(ch.y0 + k);
             int out = invalid;
             if (!reject) {
-                const int Sm = (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
-                const int Sp = (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
+                const int Sm = SDR_SOUTH_LDSU ? Sm_l : (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
+                const int Sp = SDR_SOUTH_LDSU ? Sp_l : (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
                 const int den = max(Sm + Sp - 2 * minS, 1);
                 const int qq = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
                 out = best * 16 + (((0 < best) & (best < D - 1)) ? qq : 0) + g.minD * 16;

@@ -433,6 +433,12 @@ constexpr int kSouthLAB = SDR_SOUTH_LAB;  // producer lookahead in blocks (D <= 
 #define SDR_SOUTH_PD 0  // consumer prefetch distance in blocks; 0: by register budget
 #endif
 
+#ifndef SDR_SOUTH_SOFF
+// k_south_wta producer: one resource per chain + SGPR row offset (1) or a resource per load (0).
+// Measured C2 single-stream k_south_wta 238-241 us with 1 and 229-232 us with 0 (the compiler
+// bunches the offset-addressed loads into one burst per block), so it stays off here.
+#define SDR_SOUTH_SOFF 0
+#endif
 #ifndef SDR_SOUTH_LDSU
 #define SDR_SOUTH_LDSU 1  // consumers: S row staged in LDS for subpixel + uniqueness (0: in registers)
 #endif
@@ -519,27 +525,37 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             if constexpr (SDR_SOUTH_BUF) return load_buf<K>(rsrc_at(base), lofs);
             else return load_regs<K>((const int16_t*)(base + lofs));
         };
+        // in the loop: one resource for the chain's column of C and an SGPR row offset (rows
+        // only go down, so offsets from row 0 are non-negative; see k_paths)
+        const Rsrc rC = rsrc_at(cp);
+        uint32_t soff = 0;
+        auto cload_loop = [&]() __attribute__((always_inline)) {
+            if constexpr (SDR_SOUTH_SOFF) return load_buf_so<K>(rC, lofs, soff);
+            else return cload(cp);
+        };
         // ring of 2*LA rows loaded LA ahead (see k_paths: no copies at the loop's back edge)
         Regs<K> cring[R];
 #pragma unroll
         for (int j = 0; j < LA; j++) {
             cring[j] = cload(j < naux ? abase + (ptrdiff_t)j * rowb : cp);
             cp += rowb;
+            soff += (uint32_t)rowb;
         }
         Regs<K> Lp;
 #pragma unroll
         for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
         const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
         uint32_t delta2 = path_delta0(P2x2);
-    uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
+        uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
         // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
         auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
             uint32_t* dst = &sL[bb & 1][0][lane * K];
             auto st = [&](const int, auto jc) __attribute__((always_inline)) {
                 constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
                 const Regs<K> c = cring[j];
-                cring[(j + LA) % R] = cload(cp);
+                cring[(j + LA) % R] = cload_loop();
                 cp += rowb;
+                soff += (uint32_t)rowb;
                 const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
 #pragma unroll
                 for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];

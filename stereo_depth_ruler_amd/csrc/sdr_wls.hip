@@ -138,6 +138,36 @@ __global__ __launch_bounds__(256) void k_wls_conf(const int16_t* __restrict__ dl
 // latency of the t recurrence, not a memory round trip.
 constexpr int kFgsPF = 8;
 
+#ifndef SDR_FGS_SHARED_RCP
+// the step's three divisions share one refined reciprocal (1) or are plain IEEE divisions (0):
+// bit-exact either way on MI355X, and C4 single-stream ran 800 fps with both, so the sweep's step
+// is not bound by the division chain; plain divisions stay the default
+#define SDR_FGS_SHARED_RCP 0
+#endif
+// num / den, correctly rounded, for the Thomas step's operands: |den| >= 1 (diagonally dominant
+// system) and moderate numerators, where v_div_scale leaves both operands unscaled and
+// v_div_fixup passes the quotient through.  The compiler's IEEE division is then exactly
+// rcp -> one Newton step -> q = n*r -> two residual corrections; the first three ops depend only
+// on den, so the t, p0 and p1 quotients of a step share them (and the serial t-chain loses the
+// scale and fixup ops).
+struct FgsRcp {
+    float d, r;
+};
+__device__ __forceinline__ FgsRcp fgs_rcp(float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return {d, r};
+}
+__device__ __forceinline__ float fgs_div(float n, FgsRcp R) {
+    if constexpr (!SDR_FGS_SHARED_RCP) return n / R.d;
+    float q = n * R.r;
+    float rem = __builtin_fmaf(-R.d, q, n);
+    q = __builtin_fmaf(rem, R.r, q);
+    rem = __builtin_fmaf(-R.d, q, n);
+    return __builtin_fmaf(rem, R.r, q);
+}
+
 __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1, const float* __restrict__ Cw,
                                                   float* __restrict__ T, int nlines, int n,
                                                   size_t fstride, float lam) {
@@ -177,17 +207,17 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1, const fl
                 const size_t o = (size_t)k * st;
                 if (k == 0) {
                     const float c0 = lam * rc[j];
-                    const float den = 1.0f - c0;
-                    tprev = c0 / den;
-                    p0 = r0[j] / den;
-                    if (u1) p1 = r1[j] / den;
+                    const FgsRcp den = fgs_rcp(1.0f - c0);
+                    tprev = fgs_div(c0, den);
+                    p0 = fgs_div(r0[j], den);
+                    if (u1) p1 = fgs_div(r1[j], den);
                 } else {
                     const float aa = lam * cprev;
                     const float c = lam * rc[j];
-                    const float den = (1.0f - c) - aa * (1.0f + tprev);
-                    tprev = c / den;
-                    p0 = (r0[j] - aa * p0) / den;
-                    if (u1) p1 = (r1[j] - aa * p1) / den;
+                    const FgsRcp den = fgs_rcp((1.0f - c) - aa * (1.0f + tprev));
+                    tprev = fgs_div(c, den);
+                    p0 = fgs_div(r0[j] - aa * p0, den);
+                    if (u1) p1 = fgs_div(r1[j] - aa * p1, den);
                 }
                 cprev = rc[j];
                 t[o] = tprev;

@@ -236,7 +236,9 @@ int sdr_rectify_sbs_device(sdr_rectifier* h, const uint8_t* d_sbs, size_t sbs_st
 /* Class path from the half-size gray pair already on the device (after sdr_rectify_sbs_device),
  * async on the left matcher's stream: left/right matchers (+ WLS when wls != NULL) for nframes
  * dense [F][h][w] frames.  Outputs (device, dense): d_out float disparity in px (the value
- * computeDisparity returns), d_filtered int16 (nullable), d_conf float (nullable). */
+ * computeDisparity returns), d_filtered int16 (nullable), d_conf float (nullable).  The right
+ * matcher runs on a side stream owned by the left handle, forked from and joined back to the left
+ * handle's stream with events (the call stays stream-ordered for the caller). */
 int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
                                     const uint8_t* d_small_left, const uint8_t* d_small_right,
                                     int width, int height, int nframes, float* d_out,

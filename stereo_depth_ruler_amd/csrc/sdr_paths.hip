@@ -439,6 +439,9 @@ constexpr int kSouthLAB = SDR_SOUTH_LAB;  // producer lookahead in blocks (D <= 
 // bunches the offset-addressed loads into one burst per block), so it stays off here.
 #define SDR_SOUTH_SOFF 0
 #endif
+#ifndef SDR_SOUTH_SPAD
+#define SDR_SOUTH_SPAD 4  // dword padding of the consumers' staged S rows
+#endif
 #ifndef SDR_SOUTH_LDSU
 #define SDR_SOUTH_LDSU 1  // consumers: S row staged in LDS for subpixel + uniqueness (0: in registers)
 #endif
@@ -491,7 +494,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     __shared__ uint32_t sL[2][RB][LSTR];
     // SDR_SOUTH_LDSU: each consumer row's S staged in LDS for the subpixel neighbours and the
     // uniqueness minimum (one 16-B write per lane, three masking u16 writes, one read back)
-    __shared__ uint32_t sS[SDR_SOUTH_LDSU ? kSouthConsumers : 1][4][SDR_SOUTH_LDSU ? DMAX / 2 : 1];
+    // rows padded by 4 dwords: the four lane groups' 16-B writes start on different banks
+    __shared__ uint32_t sS[SDR_SOUTH_LDSU ? kSouthConsumers : 1][4][SDR_SOUTH_LDSU ? DMAX / 2 + SDR_SOUTH_SPAD : 1];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cg = blockIdx.x;

@@ -157,3 +157,47 @@ def test_live_loop_frame_device_pipeline(oracle, cfg):
         assert np.array_equal(out[f].cpu().numpy(), df)
         ref_xyz = oracle.reproject(df, cfg.Q, False)
         assert np.array_equal(depth[f].cpu().numpy().view(np.uint32), ref_xyz.view(np.uint32))
+
+
+def test_class_path_back_to_back_on_a_side_stream(cfg):
+    """sdr_stereo_class_compute_device forks the right matcher onto the left handle's side stream
+    and joins it before the WLS filter: calls enqueued back to back on a non-default stream (no
+    host synchronisation between them) must give what the same calls give one at a time."""
+    import ctypes
+
+    from stereo_depth_ruler_amd._lib import check, lib
+    from stereo_depth_ruler_amd.ximgproc import createDisparityWLSFilter
+
+    dev = torch.device("cuda", 0)
+    r = StereoRectifier(cfg)
+    left = sdr.StereoSGBM.create(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_SGBM_3WAY)
+    right = sdr.createRightMatcher(left)
+    wls = createDisparityWLSFilter(left)
+    wls.setLambda(8000.0)
+    wls.setSigmaColor(1.1)
+    inputs = [r.rectify_sbs(torch.from_numpy(sbs_frames(1, seed=60 + i)).to(dev), bgr=False) for i in range(4)]
+    torch.cuda.synchronize()
+    F, h2, w2 = inputs[0]["small_left"].shape
+
+    def run(small, stream):
+        out = torch.empty((F, h2, w2), dtype=torch.float32, device=dev)
+        filt = torch.empty((F, h2, w2), dtype=torch.int16, device=dev)
+        check(lib().sdr_sgbm_set_stream(left._h, ctypes.c_void_p(stream.cuda_stream)))
+        check(lib().sdr_stereo_class_compute_device(left._h, right._h, wls._h, small["small_left"].data_ptr(),
+                                                    small["small_right"].data_ptr(), w2, h2, F,
+                                                    out.data_ptr(), filt.data_ptr(), None))
+        return out, filt
+
+    s0 = torch.cuda.current_stream(dev)
+    ref = []
+    for small in inputs:
+        ref.append(run(small, s0))
+        torch.cuda.synchronize()
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        got = [run(small, side) for small in inputs]
+    torch.cuda.synchronize()
+    for (ro, rf), (go, gf) in zip(ref, got):
+        assert torch.equal(rf, gf)
+        assert torch.equal(ro.view(torch.int32), go.view(torch.int32))
+    check(lib().sdr_sgbm_set_stream(left._h, ctypes.c_void_p(s0.cuda_stream)))

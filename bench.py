@@ -151,6 +151,9 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--streams", type=int, default=3, help="frames in flight (one matcher + stream each)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI) for real runs; gloo rehearses the N>1 path with every "
+                         "rank on the one GPU of a 1-GPU box (gather staged through host memory)")
     a = ap.parse_args()
 
     import torch
@@ -159,10 +162,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = a.dist_backend == "gloo"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            local = local % torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -223,7 +232,8 @@ def main():
     m = ms[0]
     gather_bufs = None
     if world > 1 and rank == 0:  # RCCL has no int16: gather the disparity bytes
-        gather_bufs = [[torch.empty(gather_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
+        gather_bufs = [[torch.empty(gather_bytes, dtype=torch.uint8, device="cpu" if gloo else dev)
+                        for _ in range(world)]
                        for _ in range(2 * ns)]
     pending = [None] * (2 * ns)
 
@@ -242,6 +252,8 @@ def main():
                 # gather this step's disparity from every rank; a later step reuses the slot only
                 # after this collective has completed
                 src = as_bytes(res) if res.dtype != torch.uint8 else res
+                if gloo:
+                    src = src.cpu()  # gloo gathers host tensors (synchronises this stream)
                 pending[slot] = dist.gather(src.reshape(-1).clone() if kind != "sgbm" else src,
                                             gather_bufs[slot] if rank == 0 else None, dst=0,
                                             async_op=True)
@@ -271,7 +283,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
@@ -380,7 +392,8 @@ def main():
             "params": dict(zip(["minDisparity", "numDisparities", "blockSize", "P1", "P2",
                                 "disp12MaxDiff", "preFilterCap", "uniquenessRatio",
                                 "speckleWindowSize", "speckleRange", "mode"], args)),
-            "parallelism": f"frame shard x{world}" + (" + RCCL gather to rank 0" if world > 1 else ""),
+            "parallelism": f"frame shard x{world}" + ((" + gloo gather to rank 0 (rehearsal)" if gloo else
+                                                      " + RCCL gather to rank 0") if world > 1 else ""),
             "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),

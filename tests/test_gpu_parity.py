@@ -60,6 +60,9 @@ CASES = [
     (70, 300, 240, 2, 5, 0, 12, (0, 0), 1, 600, 2400, 63, 15),
     (11, 60, 16, 1, 5, 0, 12, (0, 0), 1, 600, 2400, 63, 16),            # short image, HH bottom rule
     (9, 60, 16, 2, 5, 0, 12, (0, 0), 1, 600, 2400, 63, 17),             # 3WAY tiny stripes
+    (40, 200, 64, 0, 11, 0, 12, (30, 2), 1, 600, 2400, 63, 18),         # largest block (11x11)
+    (44, 210, 48, 2, 11, 0, 10, (0, 0), 1, 600, 2400, 63, 19),          # 3WAY, 11x11
+    (36, 300, 256, 0, 9, 0, 12, (0, 0), 1, 600, 2400, 63, 20),          # D = 256, 5-path
 ]
 
 

@@ -422,8 +422,12 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 // kSouthPad rows of slack instead of being clamped.
 // ------------------------------------------------------------------------------------------
 // 1 producer + 3 consumer waves (256 threads): at <= 96 VGPRs five workgroups fit a CU, so
-// the 1152 column chains of a 1280x720 d=128 frame are resident in one pass
-constexpr int kSouthConsumers = 3;
+// the 1152 column chains of a 1280x720 d=128 frame are resident in one pass.  2 and 4 consumer
+// waves measured the same within noise (C2 single-stream 240-249 us, all three bit-exact).
+#ifndef SDR_SOUTH_CONSUMERS
+#define SDR_SOUTH_CONSUMERS 3
+#endif
+constexpr int kSouthConsumers = SDR_SOUTH_CONSUMERS;
 constexpr int kSouthRB = 4 * kSouthConsumers;  // rows per block (4 per consumer wave)
 #ifndef SDR_SOUTH_LAB
 #define SDR_SOUTH_LAB 1

@@ -136,7 +136,10 @@ __global__ __launch_bounds__(256) void k_wls_conf(const int16_t* __restrict__ dl
 // moves both right-hand sides between the two (LDS tiles).  Each lane walks its line with the
 // loads of the next PF samples in flight (register ring), so a step costs the dependent-division
 // latency of the t recurrence, not a memory round trip.
-constexpr int kFgsPF = 8;
+#ifndef SDR_FGS_PF
+#define SDR_FGS_PF 8  // samples each lane loads ahead in the line solves
+#endif
+constexpr int kFgsPF = SDR_FGS_PF;
 
 #ifndef SDR_FGS_SHARED_RCP
 // the step's three divisions share one refined reciprocal (1) or are plain IEEE divisions (0):
@@ -265,6 +268,123 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1, const fl
     }
 }
 
+#ifndef SDR_FGS_V2
+#define SDR_FGS_V2 1  // branch-light line solve (0: the first version above)
+#endif
+// The same line solve without per-sample branches: the second right-hand side is a template
+// parameter, the first sample uses the general step (with cprev = tprev = p = 0 it computes
+// den = (1 - c) - 0, t = c / den, p = (r - 0) / den: the k = 0 formulas, bit for bit), and only
+// the last, partial batch of PF samples checks the line's end.
+template <bool U1>
+__global__ __launch_bounds__(64) void k_fgs_sweep2(float* U0, float* U1p, const float* __restrict__ Cw,
+                                                   float* __restrict__ T, int nlines, int n,
+                                                   size_t fstride, float lam) {
+    constexpr int PF = kFgsPF;
+    const int l = blockIdx.x * 64 + threadIdx.x;
+    if (l >= nlines) return;
+    const size_t base = (size_t)blockIdx.y * fstride + l;
+    float* u0 = U0 + base;
+    float* u1 = U1 ? U1p + base : nullptr;
+    const float* cw = Cw + base;
+    float* t = T + base;
+    const size_t st = (size_t)nlines;
+    const int last = n - 1;
+    // ---- forward elimination ----
+    float r0[PF], r1[PF], rc[PF];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const size_t o = (size_t)min(j, last) * st;
+        r0[j] = u0[o];
+        if constexpr (U1) r1[j] = u1[o];
+        rc[j] = cw[o];
+    }
+    float cprev = 0.0f, tprev = 0.0f, p0 = 0.0f, p1 = 0.0f;
+    auto fwd = [&](int k, int j) __attribute__((always_inline)) {
+        const size_t o = (size_t)k * st;
+        const float aa = lam * cprev;
+        const float c = lam * rc[j];
+        const float den = (1.0f - c) - aa * (1.0f + tprev);
+        tprev = c / den;
+        p0 = (r0[j] - aa * p0) / den;
+        if constexpr (U1) p1 = (r1[j] - aa * p1) / den;
+        cprev = rc[j];
+        t[o] = tprev;
+        u0[o] = p0;
+        if constexpr (U1) u1[o] = p1;
+    };
+    int k0 = 0;
+    for (;; k0 += PF) {
+        float n0[PF], n1[PF], nc[PF];
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const size_t o = (size_t)min(k0 + PF + j, last) * st;
+            n0[j] = u0[o];
+            if constexpr (U1) n1[j] = u1[o];
+            nc[j] = cw[o];
+        }
+        if (k0 + PF - 1 <= last) {
+#pragma unroll
+            for (int j = 0; j < PF; j++) fwd(k0 + j, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < PF; j++)
+                if (k0 + j <= last) fwd(k0 + j, j);
+        }
+        if (k0 + PF > last) break;
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            r0[j] = n0[j];
+            if constexpr (U1) r1[j] = n1[j];
+            rc[j] = nc[j];
+        }
+    }
+    // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
+    if (last < 1) return;
+    float q0 = p0, q1 = p1;
+    float b0[PF], b1[PF], bt[PF];
+#pragma unroll
+    for (int j = 0; j < PF; j++) {
+        const size_t o = (size_t)max(last - 1 - j, 0) * st;
+        b0[j] = u0[o];
+        if constexpr (U1) b1[j] = u1[o];
+        bt[j] = t[o];
+    }
+    auto bwd = [&](int k, int j) __attribute__((always_inline)) {
+        const size_t o = (size_t)k * st;
+        q0 = b0[j] - bt[j] * q0;
+        u0[o] = q0;
+        if constexpr (U1) {
+            q1 = b1[j] - bt[j] * q1;
+            u1[o] = q1;
+        }
+    };
+    for (int k1 = last - 1;; k1 -= PF) {
+        float n0[PF], n1[PF], nt[PF];
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const size_t o = (size_t)max(k1 - PF - j, 0) * st;
+            n0[j] = u0[o];
+            if constexpr (U1) n1[j] = u1[o];
+            nt[j] = t[o];
+        }
+        if (k1 - PF + 1 >= 0) {
+#pragma unroll
+            for (int j = 0; j < PF; j++) bwd(k1 - j, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < PF; j++)
+                if (k1 - j >= 0) bwd(k1 - j, j);
+        }
+        if (k1 - PF < 0) break;
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            b0[j] = n0[j];
+            if constexpr (U1) b1[j] = n1[j];
+            bt[j] = nt[j];
+        }
+    }
+}
+
 // FGS weights of one guide (per frame): ChT (column-major, for the row pass: weight between
 // (i, j) and (i, j+1) at j*h + i) and Cv (row-major, for the column pass: (i, j)-(i+1, j) at i*w + j)
 __global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__ guide, size_t gstride,
@@ -345,6 +465,16 @@ struct FgsScratch {
     float *A, *B, *T, *ChT, *Cv;
 };
 
+static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const float* Cw, float* T,
+                      int nlines, int n, size_t fs, float lam) {
+    if constexpr (SDR_FGS_V2) {
+        if (U1) hipLaunchKernelGGL((k_fgs_sweep2<true>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
+        else hipLaunchKernelGGL((k_fgs_sweep2<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
+    } else {
+        hipLaunchKernelGGL(k_fgs_sweep, grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
+    }
+}
+
 static void launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
                        float* R0, float* R1, int w, int h, int F, double lambda, double att,
                        int iters, const FgsScratch& s, hipStream_t st) {
@@ -357,12 +487,10 @@ static void launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, co
     for (int it = 0; it < iters; it++) {
         // row pass on column-major copies (lines = rows, k = column)
         hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
-        hipLaunchKernelGGL(k_fgs_sweep, dim3((h + 63) / 64, F), dim3(64), 0, st, s.A,
-                           R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
+        fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
         hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
         // column pass in place on the row-major images (lines = columns, k = row)
-        hipLaunchKernelGGL(k_fgs_sweep, dim3((w + 63) / 64, F), dim3(64), 0, st, R0, R1, s.Cv, s.T, w,
-                           h, fs, lam);
+        fgs_sweep(dim3((w + 63) / 64, F), st, R0, R1, s.Cv, s.T, w, h, fs, lam);
         lam = lam * fa;  // FastGlobalSmootherFilterImpl::filter: lambda *= lambda_attenuation
     }
 }

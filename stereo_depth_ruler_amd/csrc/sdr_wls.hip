@@ -13,7 +13,7 @@
 //   k_wls_conf     left discontinuity (inline) + discontinuity-aware LR check -> confidence
 //                  x255 (full map for getConfidenceMap) and the two FGS inputs conf*d, conf,
 //                  compacted to the ROI
-//   k_fgs_sweep    one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
+//   k_fgs_sweep(2) one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
 //                  BOTH inputs at once (the elimination coefficients depend only on the guide
 //                  and lambda).  Lane = line over k-major data (coalesced), loads PF samples
 //                  ahead in registers, so a step costs the t-recurrence's division latency

@@ -478,6 +478,26 @@ struct StampBarrier {
     }
 };
 
+#ifndef SDR_SOUTH_FLAGS
+#define SDR_SOUTH_FLAGS 0  // block hand-over by LDS counters over 3 slots (0: a barrier per block)
+#endif
+// SDR_SOUTH_FLAGS: the producer publishes "blocks staged" and each consumer "blocks consumed" in
+// LDS counters, so neither side waits for the other's slowest block as long as a slot is free.
+// Spins are bounded: a protocol error ends in wrong results (caught by the parity tests), never
+// in a wave that spins forever.  Bit-exact on MI355X but not faster (C2 single-stream 246-247 vs
+// 241-242 us with the barrier), so the barrier stays: the waits are not what bounds the pass.
+__device__ __forceinline__ void south_wait_ge(int* p, int v) {
+    for (int n = 0; n < (1 << 22); n++) {
+        const int c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (c >= v) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ void south_publish(int* p, int v, int lane) {
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int DPL, bool PAD, int NP>
 __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g, PathLaunch pl,
                                                                            SouthWtaArgs a) {
@@ -495,7 +515,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     // consumer prefetch distance in blocks: the ring (2*PD blocks) of the other directions' L
     constexpr int PD = SDR_SOUTH_PD ? SDR_SOUTH_PD : (NP * WK <= 8 ? 2 : 1);
     static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
-    __shared__ uint32_t sL[2][RB][LSTR];
+    constexpr int NB = SDR_SOUTH_FLAGS ? 3 : 2;  // LDS slots of staged L blocks
+    __shared__ uint32_t sL[NB][RB][LSTR];
+    __shared__ int s_prod, s_cons[kSouthConsumers];
     // SDR_SOUTH_LDSU: each consumer row's S staged in LDS for the subpixel neighbours and the
     // uniqueness minimum (one 16-B write per lane, three masking u16 writes, one read back)
     // rows padded by 4 dwords: the four lane groups' 16-B writes start on different banks
@@ -514,6 +536,13 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     const int last = ch.len - 1;
     const int nblk = (ch.len + RB - 1) / RB;
     StampBarrier sb;
+    if constexpr (SDR_SOUTH_FLAGS) {
+        if (threadIdx.x == 0) {
+            s_prod = 0;
+            for (int c = 0; c < kSouthConsumers; c++) s_cons[c] = 0;
+        }
+        __syncthreads();
+    }
     sb.start();
     const int stamp_slot = (blockIdx.y * gridDim.x + blockIdx.x) * (1 + kSouthConsumers) + wv;
 
@@ -557,7 +586,12 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
         // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
         auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
-            uint32_t* dst = &sL[bb & 1][0][lane * K];
+            if constexpr (SDR_SOUTH_FLAGS) {
+                if (bb >= NB)  // slot bb % NB held block bb - NB: every consumer must be done with it
+#pragma unroll
+                    for (int c = 0; c < kSouthConsumers; c++) south_wait_ge(&s_cons[c], bb - NB + 1);
+            }
+            uint32_t* dst = &sL[SDR_SOUTH_FLAGS ? bb % NB : bb & 1][0][lane * K];
             auto st = [&](const int, auto jc) __attribute__((always_inline)) {
                 constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
                 const Regs<K> c = cring[j];
@@ -569,12 +603,13 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
                 for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];
             };
             unroll_rows(st, bb * RB, std::make_integer_sequence<int, RB>{});
-            sb.sync();
+            if constexpr (SDR_SOUTH_FLAGS) south_publish(&s_prod, bb + 1, lane);
+            else sb.sync();
         };
         int b = 0;
         for (; b + NS <= nblk; b += NS) unroll_rows(block, b, std::make_integer_sequence<int, NS>{});
         unroll_rows_tail(block, b, nblk - 1, std::make_integer_sequence<int, NS - 1>{});
-        sb.sync();  // the consumers' last block
+        if constexpr (!SDR_SOUTH_FLAGS) sb.sync();  // the consumers' last block
         sb.finish(a.keys2, stamp_slot, lane);
         return;
     }
@@ -621,7 +656,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
 #pragma unroll
         for (int q = 0; q < NP; q++) oring[(s + PD) % OR][q] = oload(q, b + PD);
         // S = sat(sum of the P path costs), the fused direction's L from LDS
-        const uint32_t* ls = &sL[b & 1][r][wd0 / 2];
+        if constexpr (SDR_SOUTH_FLAGS) south_wait_ge(&s_prod, b + 1);  // block b staged
+        const uint32_t* ls = &sL[SDR_SOUTH_FLAGS ? b % NB : b & 1][r][wd0 / 2];
         Regs<WK> St;
 #pragma unroll
         for (int i = 0; i < WK; i++) {
@@ -710,9 +746,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             }
             raw[y * g.W] = (int16_t)out;
         }
-        sb.sync();
+        if constexpr (SDR_SOUTH_FLAGS) south_publish(&s_cons[wv - 1], b + 1, lane);
+        else sb.sync();
     };
-    sb.sync();  // block 0 staged
+    if constexpr (!SDR_SOUTH_FLAGS) sb.sync();  // block 0 staged
     int b = 0;
     for (; b + OR <= nblk; b += OR) unroll_rows(consume_sync, b, std::make_integer_sequence<int, OR>{});
     unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, OR - 1>{});

@@ -478,6 +478,9 @@ struct StampBarrier {
     }
 };
 
+#ifndef SDR_SOUTH_ROTATE
+#define SDR_SOUTH_ROTATE 0  // producer role rotated over the wave slots: bit-exact, no change (229-234 us)
+#endif
 #ifndef SDR_SOUTH_FLAGS
 #define SDR_SOUTH_FLAGS 0  // block hand-over by LDS counters over 3 slots (0: a barrier per block)
 #endif
@@ -523,7 +526,11 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     // rows padded by 4 dwords: the four lane groups' 16-B writes start on different banks
     __shared__ uint32_t sS[SDR_SOUTH_LDSU ? kSouthConsumers : 1][4][SDR_SOUTH_LDSU ? DMAX / 2 + SDR_SOUTH_SPAD : 1];
     const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // role of this wave (0 = producer); SDR_SOUTH_ROTATE moves the producer role to a different
+    // hardware wave slot in consecutive workgroups, so the producers of the workgroups sharing a
+    // CU do not all sit on the same SIMD if slots map to SIMDs in order
+    const int hw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = SDR_SOUTH_ROTATE ? (hw + (int)blockIdx.x) % (1 + kSouthConsumers) : hw;
     const int cg = blockIdx.x;
     const int f = blockIdx.y;
     int di = 0;

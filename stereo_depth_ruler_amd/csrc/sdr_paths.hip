@@ -4,13 +4,15 @@
 // in the kernel arguments).  One wave64 = one chain; lane l holds disparities [l*DPL, l*DPL+DPL)
 // as DPL/2 packed int16 pairs.  Per step
 //     L = C + min(Lp, min(Lp[d-1], Lp[d+1]) + P1, minLp + P2) - (minLp + P2)
-// and L is written to the direction's own buffer.  The latency-bound chains (E/W: H chains of
-// W1 steps at batch 1) overlap with the bandwidth-bound ones instead of running alone.
-// C loads are software-pipelined PF steps ahead with unconditional (clamped) addresses.
+// and L is written to the direction's own buffer (every direction but top-to-bottom).  The
+// latency-bound chains (E/W: H chains of W1 steps at batch 1) overlap with the bandwidth-bound
+// ones instead of running alone.  C loads are software-pipelined LA steps ahead through one
+// buffer resource per chain and an SGPR offset; they run into slack rows past the chain's ends
+// instead of being clamped.  The per-step minimum is a wave-uniform (SGPR) value.
 //
 // k_south_wta: the top-to-bottom chains fused with the winner-take-all (S = sat(sum_r L_r),
-// first minimum, uniqueness, subpixel, disp2 scatter); k_lr_check then applies the left-right
-// check per pixel.
+// first minimum, uniqueness, subpixel, disp2 scatter) as a producer/consumer workgroup;
+// k_lr_check then applies the left-right check per pixel.
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 

@@ -417,7 +417,9 @@ static int sgbm_rows(const uint8_t* L, const uint8_t* R, int width, int height, 
                     int minS, best, d16;
                     if (!wta_pixel(Sp, e, &minS, &best, &d16)) continue;
                     int _x2 = x + e->minX1 - best - e->minD;
-                    if (disp2cost[_x2] > minS) {
+                    /* best == -1 (every S saturated) can put _x2 one past the row: OpenCV reads */
+                    /* out of range there, but its cost MAX_COST never replaces disp2cost       */
+                    if (_x2 >= 0 && _x2 < width && disp2cost[_x2] > minS) {
                         disp2cost[_x2] = minS;
                         disp2[_x2] = (int16_t)(best + e->minD);
                     }

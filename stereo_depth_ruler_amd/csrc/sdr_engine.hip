@@ -69,6 +69,8 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     if (e->uniq >= 100) return fail(SDR_ERR_ARG, "uniquenessRatio must be < 100");
     e->disp12MaxDiff = p.disp12MaxDiff > 0 ? p.disp12MaxDiff : 1;
     e->ftzero = std::max(p.preFilterCap, 15) | 1;
+    // OpenCV's clip table is uchar: past 127 its 2*ftzero entries wrap mod 256
+    if (e->ftzero > 127) return fail(SDR_ERR_LIMIT, "preFilterCap > 127 is not supported");
     e->nstripes = p.nstripes > 0 ? p.nstripes : 4;
     e->uniq_simd = p.uniq_rule == SDR_UNIQ_SIMD ? 1
                  : p.uniq_rule == SDR_UNIQ_SCALAR ? 0
@@ -78,12 +80,34 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     e->speckle_diff = 16 * p.speckleRange;
     e->blockSize = p.blockSize;
     if (g.SH2 > 5 || g.SW2 > 5) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
-    if (g.P2 > 16383) return fail(SDR_ERR_ARG, "P2 too large for int16 path costs");
+    // The int16 domain of OpenCV's own arithmetic: C = P2 + block cost and delta = minLp + P2
+    // (minLp <= C) must fit a short.  Past it OpenCV's SIMD build wraps (short)delta0 and
+    // saturates C while its scalar build computes them in int, so the reference's output is not
+    // defined by the algorithm alone; the engine refuses instead of picking one of the two.
+    const long bmax = (long)(2 * e->ftzero + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
+    if (2L * g.P2 + bmax > 32767)
+        return fail(SDR_ERR_LIMIT, "2*P2 + (2*preFilterCap+63)*blockSize^2 exceeds the int16 cost "
+                                   "range (OpenCV's SIMD and scalar builds disagree there)");
     return SDR_OK;
 }
 
 using sdr::Buf;
 using sdr::ensure;
+
+// Frame-size limits of a matched frame (W1 > 0); host-only, shared by the enqueue and
+// sdr_sgbm_scratch_bytes.
+int check_frame(const Eff& e) {
+    const sdr::Geometry& g = e.g;
+    if (g.W1 <= 0) return SDR_OK;  // nothing matched: the output is all INVALID
+    if (g.W1 <= g.SW2) return fail(SDR_ERR_SIZE, "image too narrow for numDisparities/blockSize");
+    if (g.W > 8192) return fail(SDR_ERR_SIZE, "width > 8192 is not supported");
+    // k_paths addresses a whole chain through one buffer resource and a 32-bit SGPR offset that
+    // stays below 2^31 (num_records): the longest chain span, slack rows included, must fit
+    if ((size_t)(g.H + 2 * sdr::kSouthPad) * (size_t)(g.W1 + 1) * g.D * 2 > (size_t)INT32_MAX)
+        return fail(SDR_ERR_SIZE, "frame too large: a path chain spans more than 2 GiB of cost volume");
+    if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
+    return SDR_OK;
+}
 
 struct Stripe {
     int s0, end, out0, aux_rows, ylim;
@@ -145,7 +169,22 @@ struct sdr_sgbm {
     // class path: the right matcher runs on a side stream forked from / joined to this one
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // recorded after the last kernel that touches this handle's scratch; a stream switch makes
+    // the new stream wait for it, so one matcher used from two streams never overlaps itself
+    hipEvent_t done = nullptr;
+    bool pending = false;
 };
+
+namespace {
+void retire(sdr_sgbm* h) {
+    if (h->done && hipEventRecord(h->done, h->stream) == hipSuccess) h->pending = true;
+}
+int use_stream(sdr_sgbm* h, hipStream_t s) {
+    if (s != h->stream && h->pending) SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
+    h->stream = s;
+    return SDR_OK;
+}
+}  // namespace
 
 namespace {
 // RAII event pair around one kernel launch when per-kernel timing is on.
@@ -218,9 +257,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         if (out_min) sdr::launch_min_s16(dst, px, px, F, out_min, st);
         return SDR_OK;
     }
-    if (g.W1 <= g.SW2) return fail(SDR_ERR_SIZE, "image too narrow for numDisparities/blockSize");
-    if (W > 8192) return fail(SDR_ERR_SIZE, "width > 8192 is not supported");
-    if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
+    if ((rc = check_frame(e))) return rc;
 
     const size_t cells = (size_t)H * g.W1 * g.D;
     const int P = npaths_of(e.mode);
@@ -365,6 +402,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         sdr::launch_min_s16(dst, px, px, F, out_min, st);
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
+    retire(h);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -421,6 +459,7 @@ int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out) {
     }
     h->stream = h->own_stream;
     for (auto& ev : h->ev) (void)hipEventCreate(&ev);
+    (void)hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
     *out = h;
     return SDR_OK;
 }
@@ -440,6 +479,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->fork) (void)hipEventDestroy(h->fork);
     if (h->join) (void)hipEventDestroy(h->join);
+    if (h->done) (void)hipEventDestroy(h->done);
     if (h->side) (void)hipStreamDestroy(h->side);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -460,14 +500,14 @@ int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p) {
 
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
-    h->stream = (hipStream_t)stream;  // NULL = the HIP null (legacy default) stream
-    return SDR_OK;
+    (void)hipSetDevice(h->device);
+    return use_stream(h, (hipStream_t)stream);  // NULL = the HIP null (legacy default) stream
 }
 
 int sdr_sgbm_reset_stream(sdr_sgbm* h) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
-    h->stream = h->own_stream;
-    return SDR_OK;
+    (void)hipSetDevice(h->device);
+    return use_stream(h, h->own_stream);
 }
 
 void* sdr_sgbm_get_stream(const sdr_sgbm* h) { return h ? (void*)h->stream : nullptr; }
@@ -495,7 +535,7 @@ int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, flo
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes) {
     if (!p) return 0;
     Eff e;
-    if (make_eff(*p, width, height, &e)) return 0;
+    if (make_eff(*p, width, height, &e) || check_frame(e)) return 0;
     std::vector<Stripe> st;
     return scratch_bytes(e, std::max(nframes, 1), &st);
 }
@@ -524,6 +564,7 @@ int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, i
         for (int f = 0; f < F; f++)
             SDR_HIP(hipMemcpy2DAsync(dDisp + f * disp_fstride, disp_stride * 2, fin + f * px, W * 2,
                                      W * 2, H, hipMemcpyDeviceToDevice, h->stream));
+        retire(h);
     }
     return SDR_OK;
 }
@@ -546,6 +587,7 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint
         sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, mins, dXYZ, (size_t)W * 3,
                                   px * 3, F, h->stream);
     }
+    retire(h);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -714,10 +756,12 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
         SDR_HIP(hipEventRecord(left->fork, st));
         SDR_HIP(hipStreamWaitEvent(left->side, left->fork, 0));
         hipStream_t rs = right->stream;
-        right->stream = left->side;
+        if ((rc = use_stream(right, left->side))) return rc;
         rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
-        right->stream = rs;
+        retire(right);
+        const int rc2 = use_stream(right, rs);
         if (rc) return rc;
+        if (rc2) return rc2;
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
     if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
@@ -736,6 +780,7 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
     }
     // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34)
     sdr::launch_disp16_to_f32(res, d_out, F * px2, st);
+    retire(left);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }

@@ -743,7 +743,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         if (gl == 0 && rowok) {
             const size_t y = (size_t)(ch.y0 + k);
             int out = invalid;
-            if (!reject) {
+            // every S saturated: OpenCV's first-minimum scan (strict '<' from MAX_COST) keeps
+            // bestDisp = -1, whose value (-1 + minD) * 16 is INVALID and whose disp2 candidate
+            // (cost MAX_COST) never replaces the initial one
+            if (!reject && minS < kMaxCost) {
                 const int Sm = SDR_SOUTH_LDSU ? Sm_l : (int)(short)((dm & 1) ? (am >> 16) : (am & 0xffff));
                 const int Sp = SDR_SOUTH_LDSU ? Sp_l : (int)(short)((dp & 1) ? (ap >> 16) : (ap & 0xffff));
                 const int den = max(Sm + Sp - 2 * minS, 1);

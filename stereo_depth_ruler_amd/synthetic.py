@@ -89,6 +89,48 @@ def shifted_pair(h: int, w: int, shift: int, seed: int = 0):
     return left, right
 
 
+ADVERSARIAL_KINDS = ("noise", "binary", "steps", "periodic", "flat", "textured")
+
+
+def adversarial_pair(kind: str, h: int, w: int, num_disp: int = 16, seed: int = 0):
+    """Pairs that push the int16 cost arithmetic to its edges (parity tests only):
+
+    * noise: independent uniform noise left and right (large block costs, no true match);
+    * binary: independent 0/255 pixels (the largest BT cost per pixel, so C, L_r and the
+      saturated S sum reach their maxima);
+    * steps: 0/255 vertical bars of random widths, identical rows (ties along x, flat columns);
+    * periodic: a horizontal period dividing the disparity range, the right view shifted by a
+      whole period (several disparities match exactly: first-minimum ties, uniqueness at equality);
+    * flat: one constant grey level (every cost equal);
+    * textured: the section 8d pair (make_pair)."""
+    rng = np.random.default_rng(seed)
+    if kind == "noise":
+        return (rng.integers(0, 256, (h, w), dtype=np.uint8),
+                rng.integers(0, 256, (h, w), dtype=np.uint8))
+    if kind == "binary":
+        return (rng.integers(0, 2, (h, w), dtype=np.uint8) * 255,
+                rng.integers(0, 2, (h, w), dtype=np.uint8) * 255)
+    if kind == "steps":
+        edges = np.cumsum(rng.integers(1, 9, size=w + 1))
+        bars = (np.searchsorted(edges, np.arange(w + 8), side="right") & 1).astype(np.uint8) * 255
+        left = np.tile(bars[:w], (h, 1))
+        s = int(rng.integers(1, max(2, min(num_disp, 8))))
+        return left, np.tile(bars[s:s + w], (h, 1))
+    if kind == "periodic":
+        period = int(rng.choice([2, 4, 8]))
+        base = rng.integers(0, 256, size=period).astype(np.uint8)
+        row = base[np.arange(w + period) % period]
+        left = np.tile(row[:w], (h, 1))
+        return left, np.tile(row[period:period + w], (h, 1))
+    if kind == "flat":
+        v = np.uint8(rng.integers(0, 256))
+        return np.full((h, w), v, np.uint8), np.full((h, w), v, np.uint8)
+    if kind == "textured":
+        left, right, _ = make_pair(h, w, max(num_disp, 16), seed=seed)
+        return left, right
+    raise ValueError(kind)
+
+
 def sbs_bgr_frame(h: int, w: int, num_disp: int, seed: int = 0):
     """A ZED2-style side-by-side BGR frame (2w x h x 3) with gray replicated over channels."""
     left, right, _ = make_pair(h, w, num_disp, seed)

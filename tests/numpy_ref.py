@@ -73,6 +73,199 @@ def cost_volume(L, R, minD, D, bs, P2, ftzero, hh=False):
     return (C + P2).astype(np.int16)
 
 
+# ---- StereoSGBM A.4-A.9: a materialised-volume formulation ----
+#
+# A second, structurally different statement of the SGM core, written from the published rules
+# and not from oracle/sgbm_oracle.c: the cost volume is a direct (non-running) box sum, every path
+# direction is its own full [H][W1][D] volume computed in int64 with no int16 storage, S is an
+# explicit saturated sum, and the WTA / uniqueness / subpixel / disp2 / LR rules are vectorised over
+# whole rows.  The oracle instead follows OpenCV's row drivers (ring buffers, running sums, packed
+# per-pixel loops).  Agreement between the two pins the oracle's transcription of A.4-A.9.
+
+SGM_SGBM, SGM_HH, SGM_3WAY = 0, 1, 2
+_BIG = 1 << 40  # the d = -1 / d = D neighbours: never the minimum
+
+# predecessor offsets: the predecessor of (x, y) along r is (x - dx, y - dy)
+SGM_DIRS = {
+    SGM_SGBM: [(1, 0), (1, 1), (0, 1), (-1, 1), (-1, 0)],
+    SGM_HH: [(1, 0), (1, 1), (0, 1), (-1, 1), (-1, 0), (-1, -1), (0, -1), (1, -1)],
+    SGM_3WAY: [(1, 0), (-1, 0), (0, 1)],
+}
+
+
+def sgm_effective(minD, D, bs, P1, P2, d12, cap, uniq, mode, uniq_rule=0):
+    """OpenCV's parameter defaulting (StereoSGBM::create / computeDisparitySGBM /
+    SGBM3WayMainLoop): returns a dict of the values the algorithm actually uses."""
+    if mode == SGM_3WAY:
+        sw2 = bs // 2 if bs > 0 else 1
+    else:
+        sw2 = (bs if bs > 0 else 5) // 2
+    p1 = P1 if P1 > 0 else 2
+    p2 = max(P2 if P2 > 0 else 5, p1 + 1)
+    u = uniq if uniq >= 0 else 10
+    simd = {1: False, 2: True}.get(uniq_rule, mode == SGM_3WAY)
+    return dict(minD=minD, D=D, maxD=minD + D, SW2=sw2, SH2=sw2, P1=p1, P2=p2,
+                d12=d12 if d12 > 0 else 1, ftzero=max(cap, 15) | 1, uniq=u, simd=simd, bs=bs)
+
+
+def _box_rows(hs, s0, end, SH2, hh_bottom):
+    """Box-summed rows [s0, end) of a chain whose vertical window clamps at s0 (top) and H-1
+    (bottom); rows whose window would pass the bottom repeat the last full window (or, for
+    MODE_HH's full-DP buffer, stay 0)."""
+    H = hs.shape[0]
+    out = np.zeros((end - s0,) + hs.shape[1:], np.int64)
+    ylim = max(H - 1 - SH2, s0)
+    for y in range(s0, end):
+        if hh_bottom and y > 0 and y + SH2 >= H:
+            continue
+        t = min(y, ylim)
+        rows = np.clip(np.arange(t - SH2, t + SH2 + 1), s0, H - 1)
+        out[y - s0] = hs[rows].sum(0)
+    return out
+
+
+def _path_volume(C, dx, dy, P1, P2):
+    """L_r(p, d) = C(p, d) + min(Lp(d), Lp(d-1) + P1, Lp(d+1) + P1, minLp + P2) - (minLp + P2),
+    with Lp the predecessor's L (0 and minLp = 0 before a chain's first pixel), as a full volume."""
+    H, W1, D = C.shape
+    L = np.zeros_like(C)
+
+    def step(c, lp, mlp):
+        delta = (mlp + P2)[..., None]
+        pad = np.full(lp.shape[:-1] + (D + 2,), _BIG, np.int64)
+        pad[..., 1:-1] = lp
+        nb = np.minimum(pad[..., :-2], pad[..., 2:]) + P1
+        return c + np.minimum(np.minimum(lp, nb), delta) - delta
+
+    if dy == 0:
+        lp = np.zeros((H, D), np.int64)
+        for x in (range(W1) if dx > 0 else range(W1 - 1, -1, -1)):
+            L[:, x] = step(C[:, x], lp, lp.min(-1))  # zeros before the first pixel: minLp = 0
+            lp = L[:, x]
+        return L
+    src = np.arange(W1) - dx
+    ok = (src >= 0) & (src < W1)
+    prev = None
+    for y in (range(H) if dy > 0 else range(H - 1, -1, -1)):
+        lp = np.zeros((W1, D), np.int64)
+        mlp = np.zeros(W1, np.int64)
+        if prev is not None:
+            lp[ok] = prev[src[ok]]
+            mlp[ok] = prev[src[ok]].min(-1)
+        L[y] = step(C[y], lp, mlp)
+        prev = L[y]
+    return L
+
+
+def _c_div(n, d):
+    """C integer division (truncation toward zero), d > 0."""
+    return np.sign(n) * (np.abs(n) // d)
+
+
+def _wta_rows(S, e, W, minX1):
+    """A.8 + A.9 on saturated sums S [rows][W1][D] -> disparity rows [rows][W] (1/16 px)."""
+    rows, W1, D = S.shape
+    inv = (e["minD"] - 1) * 16
+    out = np.full((rows, W), inv, np.int64)
+    best = S.argmin(-1)  # first minimum
+    minS = S.min(-1)
+    dd = np.arange(D)
+    far = np.abs(dd[None, None, :] - best[..., None]) > 1
+    if e["simd"]:
+        if e["uniq"] > 0:
+            thr = (100 * minS) // (100 - e["uniq"]) + 1
+            thr = ((thr + 32768) % 65536) - 32768  # (short)(thresh + 1)
+            reject = ((S < thr[..., None]) & far).any(-1)
+        else:
+            reject = np.zeros(best.shape, bool)
+    else:
+        reject = ((S * (100 - e["uniq"]) < minS[..., None] * 100) & far).any(-1)
+    # the first-minimum scan starts from (MAX_COST, bestDisp = -1) with a strict '<': a pixel whose
+    # every S saturated keeps bestDisp = -1, i.e. the value (-1 + minD) * 16 = INVALID, and its
+    # disp2 candidate (cost MAX_COST) never replaces the initial one
+    reject |= minS >= 32767
+    inner = (best > 0) & (best < D - 1)
+    bm = np.clip(best - 1, 0, D - 1)
+    bp = np.clip(best + 1, 0, D - 1)
+    Sm = np.take_along_axis(S, bm[..., None], -1)[..., 0]
+    Sp = np.take_along_axis(S, bp[..., None], -1)[..., 0]
+    den = np.maximum(Sm + Sp - 2 * minS, 1)
+    d16 = best * 16 + np.where(inner, _c_div((Sm - Sp) * 16 + den, 2 * den), 0) + e["minD"] * 16
+    xs = np.arange(W1)
+    for r in range(rows):
+        acc = ~reject[r]
+        out[r, minX1 + xs[acc]] = d16[r, acc]
+        # disp2: right-view WTA; per target column the smallest minS wins, ties -> the largest x
+        # (OpenCV scans x descending and replaces only on a strictly smaller cost)
+        disp2 = np.full(W, inv, np.int64)
+        xa = xs[acc]
+        x2 = xa + minX1 - best[r, acc] - e["minD"]
+        inr = (x2 >= 0) & (x2 < W)
+        xa, x2, ms, b = xa[inr], x2[inr], minS[r, acc][inr], best[r, acc][inr]
+        order = np.lexsort((-xa, ms, x2))
+        first = np.ones(order.size, bool)
+        first[1:] = x2[order][1:] != x2[order][:-1]
+        win = order[first]
+        disp2[x2[win]] = b[win] + e["minD"]
+        # A.9: invalidate when both floor/ceil correspondences disagree by more than disp12MaxDiff
+        d1 = out[r]
+        xx = np.arange(W)
+        chk = (xx >= minX1) & (xx < minX1 + W1) & (d1 != inv)
+        lo, hi = d1 >> 4, (d1 + 15) >> 4
+        bad = np.ones(W, bool)
+        for dv in (lo, hi):
+            xs2 = xx - dv
+            inb = (xs2 >= 0) & (xs2 < W)
+            t = disp2[np.clip(xs2, 0, W - 1)]
+            bad &= inb & (t >= e["minD"]) & (np.abs(t - dv) > e["d12"])
+        out[r, chk & bad] = inv
+    return out
+
+
+def sgm_full_volume(L, R, minD, D, bs, P1, P2, d12, cap, uniq, ws=0, sr=0, mode=SGM_SGBM,
+                    nstripes=4, uniq_rule=0, stages=3):
+    """StereoSGBM::compute as a materialised-volume formulation.  stages: 1 median, 2 speckle."""
+    e = sgm_effective(minD, D, bs, P1, P2, d12, cap, uniq, mode, uniq_rule)
+    H, W = L.shape
+    minX1, maxX1 = max(e["maxD"], 0), W + min(minD, 0)
+    W1 = maxX1 - minX1
+    inv = (minD - 1) * 16
+    if W1 <= 0:
+        return np.full((H, W), inv, np.int16)
+    pix = bt_cost_volume_rows(L, R, minD, D, e["ftzero"]).astype(np.int64)
+    s = e["SW2"]
+    xi = np.clip(np.arange(W1)[:, None] + np.arange(-s, s + 1)[None, :], 0, W1 - 1)
+    hs = pix[:, xi, :].sum(2)
+    if mode == SGM_3WAY:
+        segs = []
+        sz = int(np.ceil(H / nstripes))
+        overlap = (bs // 2 + 1) + int(np.ceil(0.1 * sz))
+        for k in range(nstripes):
+            if k * sz >= H:
+                break
+            segs.append((max(min(k * sz - overlap, H), 0), min((k + 1) * sz, H), k * sz))
+    else:
+        segs = [(0, H, 0)]
+    raw = np.full((H, W), inv, np.int64)
+    for s0, end, out0 in segs:
+        C = e["P2"] + _box_rows(hs, s0, end, e["SH2"], mode == SGM_HH)
+        assert C.max() <= 32767, "outside the int16 cost domain"
+        Ssum = np.zeros_like(C)
+        for dx, dy in SGM_DIRS[mode]:
+            Lr = _path_volume(C, dx, dy, e["P1"], e["P2"])
+            assert Lr.min() >= 0 and Lr.max() <= 32767
+            Ssum += Lr
+        Ssum = np.minimum(Ssum, 32767)
+        raw[out0:end] = _wta_rows(Ssum[out0 - s0:], e, W, minX1)
+    out = raw.astype(np.int16)
+    if stages & 1:
+        from scipy.ndimage import median_filter
+        out = median_filter(out, size=3, mode="nearest")
+    if (stages & 2) and ws > 0:
+        out = speckle_filter(out, inv, ws, 16 * sr)
+    return out
+
+
 def speckle_filter(img, new_val, max_size, max_diff):
     """Components by BFS over 4-neighbours joined when both != new_val and |diff| <= max_diff."""
     H, W = img.shape

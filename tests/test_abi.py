@@ -118,3 +118,30 @@ def test_wls_params_for_sgbm_matches_ximgproc(oracle):
         assert (p.lrc_thresh, p.num_iter, p.min_disp) == (q.lrc_thresh, q.num_iter, q.min_disp)
         assert (p.lambda_, p.sigma_color, p.lambda_attenuation) == (q.lambda_, q.sigma_color, q.lambda_attenuation)
         assert abs(p.roll_off - 0.001) < 1e-9
+
+
+def test_int16_domain_guard_host_only():
+    """P2 is bounded by 2*P2 + (2*ftzero+63)*blockSize^2 <= 32767 (OpenCV's SIMD and scalar
+    builds disagree past it); checked on the host, before any device work."""
+    from test_oracle_sgm_volume import p2_domain_max
+
+    L = _lib.lib()
+    for bs, cap, mode in ((5, 63, 0), (11, 63, 1), (1, 15, 2), (7, 127, 0)):
+        pmax = p2_domain_max(bs, cap, mode)
+        ok = _lib.SgbmParams(0, 64, bs, 10, pmax, 1, cap, 10, 0, 0, mode, 4, 0)
+        assert L.sdr_sgbm_scratch_bytes(ctypes.byref(ok), 320, 100, 1) > 0
+        bad = _lib.SgbmParams(0, 64, bs, 10, pmax + 1, 1, cap, 10, 0, 0, mode, 4, 0)
+        assert L.sdr_sgbm_scratch_bytes(ctypes.byref(bad), 320, 100, 1) == 0
+        assert b"int16" in L.sdr_last_error()
+    big = _lib.SgbmParams(0, 64, 5, 10, 100, 1, 128, 10, 0, 0, 0, 4, 0)
+    assert L.sdr_sgbm_scratch_bytes(ctypes.byref(big), 320, 100, 1) == 0  # preFilterCap > 127
+
+
+def test_chain_span_guard_host_only():
+    """k_paths addresses a chain with a 32-bit offset: frames whose chain span passes 2 GiB are
+    refused (SDR_ERR_SIZE) instead of silently reading zeros."""
+    L = _lib.lib()
+    p = _lib.SgbmParams(0, 256, 5, 600, 2400, 1, 63, 12, 0, 0, 1, 4, 0)
+    assert L.sdr_sgbm_scratch_bytes(ctypes.byref(p), 1920, 1080, 1) > 0  # C5 fits
+    assert L.sdr_sgbm_scratch_bytes(ctypes.byref(p), 8192, 1200, 1) == 0
+    assert b"2 GiB" in L.sdr_last_error()

@@ -1,0 +1,121 @@
+"""Adversarial and hypothesis-driven GPU parity, bit-exact against
+the oracle: random sizes, disparity ranges (D in 16Z up to 256, minDisparity < 0), all three modes,
+every block size, P1 < P2 up to the int16 domain bound, both uniqueness rules, 3WAY stripe counts,
+speckle on/off -- on inputs built to reach the int16 edges where a packed-int16 GPU formulation and
+a scalar restatement can part ways: saturated S sums (every disparity at 32767), first-minimum ties
+(periodic textures), uniqueness at equality, 0/255 steps and textureless frames."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+import stereo_depth_ruler_amd as sdr  # noqa: E402
+from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+from test_oracle_sgm_volume import p2_domain_max  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def check_case(oracle, kind, H, W, args, nstripes=4, uniq_rule=0, seed=0):
+    L, R = S.adversarial_pair(kind, H, W, args[1], seed=seed)
+    m = sdr.StereoSGBM.create(*args, nstripes=nstripes, uniq_rule=uniq_rule)
+    got = m.compute(L, R)
+    p = oracle.make_params(*args, nstripes=nstripes, uniq_rule=uniq_rule)
+    ref = oracle.sgbm_compute(L, R, p)
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} px differ"
+    # the LR-checked map before median/speckle as well
+    raw = m.debug_stage(2, (H, W), np.int16)
+    assert np.array_equal(raw, oracle.sgbm_compute(L, R, p, stages=0))
+    m.close()
+
+
+@st.composite
+def sgbm_cases(draw):
+    mode = draw(st.sampled_from([0, 1, 2]))
+    D = 16 * draw(st.integers(1, 16))
+    bs = draw(st.sampled_from([1, 3, 5, 7, 9, 11]))
+    minD = draw(st.integers(-40, 8))
+    H = draw(st.integers(4, 48))
+    W1 = draw(st.integers(bs // 2 + 1, 160))  # matched columns (0 < W1 <= SW2 is an OpenCV error)
+    W = W1 - min(minD, 0) + max(minD + D, 0)
+    cap = draw(st.sampled_from([c for c in (15, 31, 63, 127) if p2_domain_max(bs, c, mode) >= 64]))
+    pmax = p2_domain_max(bs, cap, mode)
+    P1 = draw(st.integers(1, max(1, min(pmax - 1, 2000))))
+    P2 = draw(st.one_of(st.just(pmax), st.integers(P1 + 1, max(P1 + 1, pmax))))
+    uniq = draw(st.sampled_from([0, 1, 5, 10, 15, 50]))
+    ws = draw(st.sampled_from([0, 0, 10, 100]))
+    sr = draw(st.integers(1, 4))
+    d12 = draw(st.sampled_from([1, 2, 5, 1000000]))
+    kind = draw(st.sampled_from(S.ADVERSARIAL_KINDS))
+    return dict(kind=kind, H=H, W=W, args=(minD, D, bs, P1, P2, d12, cap, uniq, ws, sr, mode),
+                nstripes=draw(st.sampled_from([1, 2, 3, 4, 8])), uniq_rule=draw(st.integers(0, 2)),
+                seed=draw(st.integers(0, 10**6)))
+
+
+@settings(max_examples=80, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(case=sgbm_cases())
+def test_hypothesis_bit_exact(oracle, case):
+    check_case(oracle, case["kind"], case["H"], case["W"], case["args"], case["nstripes"],
+               case["uniq_rule"], case["seed"])
+
+
+# Deterministic edge cases at medium size (every mode, both int16 extremes of the domain).
+EDGE = [
+    # kind, H, W, (minD, D, bs, P1, P2, d12, cap, uniq, ws, sr, mode)
+    ("binary", 40, 300, (0, 128, 11, 81, p2_domain_max(11, 63, 1), 1, 63, 10, 0, 0, 1)),
+    ("binary", 40, 300, (-3, 48, 11, 81, p2_domain_max(11, 63, 0), 1000000, 63, 5, 0, 0, 0)),
+    ("binary", 40, 300, (0, 64, 11, 81, p2_domain_max(11, 63, 2), 1, 63, 15, 0, 0, 2)),
+    ("noise", 64, 400, (0, 256, 9, 300, p2_domain_max(9, 63, 1), 1, 63, 12, 100, 2, 1)),
+    ("noise", 64, 400, (-79, 80, 5, 600, p2_domain_max(5, 63, 2), 1000000, 63, 0, 0, 2, 2)),
+    ("periodic", 32, 256, (0, 64, 3, 8, 32, 1, 63, 0, 0, 0, 0)),
+    ("periodic", 32, 256, (0, 64, 1, 1, 2, 1, 15, 15, 50, 1, 1)),
+    ("steps", 48, 320, (0, 96, 5, 600, 2400, 1, 63, 12, 200, 2, 0)),
+    ("steps", 48, 320, (0, 96, 7, 50, 12000, 2, 31, 10, 30, 1, 2)),
+    ("flat", 30, 200, (0, 32, 5, 600, 2400, 1, 63, 12, 0, 0, 0)),
+    ("flat", 30, 200, (0, 32, 5, 600, 2400, 1, 63, 0, 0, 0, 2)),
+    ("textured", 90, 420, (0, 128, 11, 200, p2_domain_max(11, 63, 0), 1, 63, 12, 200, 2, 0)),
+]
+
+
+@pytest.mark.parametrize("kind,H,W,args", EDGE, ids=[f"{e[0]}_m{e[3][10]}_bs{e[3][2]}_P2{e[3][4]}" for e in EDGE])
+def test_edge_cases_bit_exact(oracle, kind, H, W, args):
+    for rule in (0, 1, 2):
+        check_case(oracle, kind, H, W, args, uniq_rule=rule, seed=H * W)
+
+
+def test_outside_int16_domain_is_refused():
+    L = np.zeros((20, 100), np.uint8)
+    pmax = p2_domain_max(5, 63, 0)
+    sdr.StereoSGBM.create(0, 16, 5, 10, pmax, 1, 63).compute(L, L)
+    with pytest.raises(sdr.SDRError) as e:
+        sdr.StereoSGBM.create(0, 16, 5, 10, pmax + 1, 1, 63).compute(L, L)
+    assert e.value.code == -8
+
+
+def test_one_matcher_two_streams(oracle):
+    """A matcher used back to back from two torch streams: the handle orders the second stream
+    after the first one's use of its scratch (no overlap, no corruption)."""
+    dev = torch.device("cuda", 0)
+    args = (0, 64, 5, 600, 2400, 1, 63, 12, 100, 2, 0)
+    m = sdr.StereoSGBM.create(*args)
+    pairs = [S.make_pair(200, 480, 64, seed=60 + i)[:2] for i in range(4)]
+    dl = [(torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)) for a, b in pairs]
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = []
+    for i, (a, b) in enumerate(dl):
+        with torch.cuda.stream(s1 if i % 2 == 0 else s2):
+            outs.append(m.compute(a, b))
+    torch.cuda.synchronize(dev)
+    p = oracle.make_params(*args)
+    for (a, b), o in zip(pairs, outs):
+        assert np.array_equal(o.cpu().numpy(), oracle.sgbm_compute(a, b, p))

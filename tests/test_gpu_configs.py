@@ -1,0 +1,118 @@
+"""BASELINE.json's full-size GPU configs under bit-exact parity.
+
+* C5 (configs[4]): one 3840x1080 side-by-side BGR frame through ``pipeline.CloudEmit``, the
+  point_cloud/src/pcd_write.cpp:81-141 chain at 1920x1080, d=256, MODE_HH: split -> BGR2GRAY ->
+  StereoSGBM::compute -> /16 -> reprojectImageTo3D(handleMissing) -> convertCVMatToPCL(left) ->
+  VoxelGrid -> savePCDFileBinary.  Disparity, XYZ, the organised cloud and the PCD bytes are
+  compared with the oracle chain, with the reference's 5 mm leaf (on a millimetre cloud PCL's
+  int64 overflow test wraps, so passthrough or not depends on the cloud) and with a leaf that does
+  not overflow, so the voxel sort and centroid path runs on the ~2 M-point cloud.
+* C3 (configs[2]): 32 distinct 1280x720 pairs, d=256, MODE_HH in ONE batched device call; frames
+  0, 15 and 31 against the oracle, all 32 against single-frame device runs.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import stereo_depth_ruler_amd as sdr  # noqa: E402
+from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+from stereo_depth_ruler_amd.cloud import pcd_header, savePCDFileBinary  # noqa: E402
+from stereo_depth_ruler_amd.pipeline import CloudEmit  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def u32(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+C5_ARGS = (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_HH)
+
+
+@pytest.fixture(scope="module")
+def c5_run(oracle):
+    W, H = 1920, 1080
+    frame = S.sbs_bgr_color_frame(H, W, 256, seed=500)  # (H, 2W, 3)
+    dev = torch.device("cuda", 0)
+    sbs = torch.from_numpy(frame).to(dev).unsqueeze(0)
+    pipe = CloudEmit(W, H, C5_ARGS, 1, S.REFERENCE_Q, leaf=0.005)
+    stream = torch.cuda.current_stream(dev)
+    pipe.enqueue(sbs, stream, voxel=False)
+    torch.cuda.synchronize(dev)
+    disp = pipe.disp[0].cpu().numpy()
+    xyz = pipe.xyz[0].cpu().numpy()
+    points = pipe.points[0].cpu().numpy()
+    left, right = frame[:, :W], frame[:, W:]
+    gl, gr = oracle.bgr2gray(left), oracle.bgr2gray(right)
+    ref = oracle.sgbm_compute(gl, gr, oracle.make_params(*C5_ARGS))
+    rxyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, True)
+    rpts = oracle.xyz_to_cloud(rxyz, left)
+    yield dict(pipe=pipe, disp=disp, xyz=xyz, points=points, ref=ref, rxyz=rxyz, rpts=rpts)
+    pipe.close()
+
+
+def test_c5_disparity_xyz_cloud_bit_exact(c5_run):
+    r = c5_run
+    assert np.array_equal(r["disp"], r["ref"]), f"{(r['disp'] != r['ref']).sum()} px differ"
+    assert np.array_equal(u32(r["xyz"]), u32(r["rxyz"]))
+    assert np.array_equal(u32(r["points"]), u32(r["rpts"]))
+    assert (r["ref"] > -16).mean() > 0.7  # the synthetic scene is mostly matched
+
+
+@pytest.mark.parametrize("leaf", [0.005, None])
+def test_c5_voxel_grid_at_size(oracle, c5_run, tmp_path, leaf):
+    """leaf 0.005: the reference's own leaf on a millimetre cloud.
+    leaf None: the smallest of 50/100/200/400 mm that does not overflow PCL's int32 voxel index,
+    so the sort + centroid reduction runs on the full cloud."""
+    rpts = c5_run["rpts"]
+    if leaf is None:
+        for cand in (50.0, 100.0, 200.0, 400.0):
+            ref, passthrough = oracle.voxel_grid(rpts, cand)
+            if not passthrough:
+                leaf = cand
+                break
+        assert leaf is not None and ref.shape[0] < rpts.shape[0] // 4
+    else:
+        # PCL's overflow test on (dx*dy*dz) in int64 wraps on millimetre clouds, so whether this is
+        # a passthrough depends on the cloud's extent; the engine must agree either way
+        ref, passthrough = oracle.voxel_grid(rpts, leaf)
+    vg = sdr.cloud.VoxelGrid()
+    vg.setLeafSize(leaf, leaf, leaf)
+    cloud = sdr.cloud.PointCloud(c5_run["pipe"].points[0], 1920, 1080)
+    out = vg.filter(cloud)
+    assert vg.passthrough == passthrough
+    got = out.points.cpu().numpy()
+    assert np.array_equal(u32(got), u32(ref)), (got.shape, ref.shape)
+    path = tmp_path / "frame.pcd"
+    savePCDFileBinary(path, out)
+    w, h = (1920, 1080) if passthrough else (ref.shape[0], 1)
+    assert path.read_bytes() == pcd_header(w, h) + ref.tobytes()
+
+
+def test_c3_batch32_hh_d256(oracle):
+    H, W, F = 720, 1280, 32
+    args = (0, 256, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_HH)
+    Ls, Rs = S.make_batch(F, H, W, 256, seed0=0)
+    dev = torch.device("cuda", 0)
+    m = sdr.StereoSGBM.create(*args)
+    out = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    with ThreadPoolExecutor(3) as ex:  # ctypes releases the GIL: the three oracle frames overlap
+        refs = list(ex.map(lambda i: oracle.sgbm_compute(Ls[i], Rs[i], p), (0, 15, 31)))
+    for i, ref in zip((0, 15, 31), refs):
+        assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
+    m1 = sdr.StereoSGBM.create(*args)
+    for i in range(F):
+        single = m1.compute(torch.from_numpy(Ls[i]).to(dev)[None], torch.from_numpy(Rs[i]).to(dev)[None])
+        assert np.array_equal(out[i], single[0].cpu().numpy()), f"frame {i} differs from its single-frame run"
+    m.close()
+    m1.close()

@@ -1,0 +1,86 @@
+"""Pins the oracle's SGM core with a second, independent formulation.
+
+oracle/sgbm_oracle.c follows OpenCV's row drivers: ring buffers of path costs, running box sums,
+per-pixel loops, the 3WAY stripe loop.  tests/numpy_ref.sgm_full_volume states the same rules as
+whole-volume numpy: direct box sums, one materialised int64 volume per path direction, an explicit
+saturated S, and row-vectorised first-minimum WTA, both uniqueness forms, subpixel, the disp2
+scatter and the LR check.  The cases are seeded and cover all three modes, 3WAY stripe counts,
+both uniqueness rules, minDisparity < 0, every block size, P2 up to the int16 domain bound the
+engine enforces, and the adversarial inputs of synthetic.adversarial_pair (saturated S sums,
+first-minimum ties, uniqueness at equality, textureless rows).
+"""
+import numpy as np
+import pytest
+
+import numpy_ref as N
+from stereo_depth_ruler_amd import synthetic as S
+
+
+def p2_domain_max(bs, cap, mode):
+    """Largest P2 the engine accepts: 2*P2 + (2*ftzero+63)*(2*SW2+1)^2 <= 32767."""
+    ft = max(cap, 15) | 1
+    sw2 = (bs // 2 if bs > 0 else 1) if mode == 2 else (bs if bs > 0 else 5) // 2
+    return (32767 - (2 * ft + 63) * (2 * sw2 + 1) ** 2) // 2
+
+
+def random_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    mode = seed % 3
+    D = int(rng.choice([16, 32, 48]))
+    bs = int(rng.choice([1, 3, 5, 7, 9, 11]))
+    minD = int(rng.integers(-20, 6))
+    H = int(rng.integers(6, 36))
+    W = int(rng.integers(D + max(minD, 0) + bs + 4, D + 96))
+    cap = int(rng.choice([15, 31, 63]))
+    p2max = p2_domain_max(bs, cap, mode)
+    P1 = int(rng.integers(1, 300))
+    P2 = p2max if seed % 4 == 0 else int(rng.integers(P1 + 1, max(P1 + 2, min(p2max, 4000))))
+    uniq = int(rng.choice([0, 5, 10, 15]))
+    ws, sr = [(0, 0), (20, 1), (50, 2)][seed % 3]
+    d12 = int(rng.choice([1, 2, 1000000]))
+    kind = S.ADVERSARIAL_KINDS[seed % len(S.ADVERSARIAL_KINDS)]
+    return dict(kind=kind, H=H, W=W, args=(minD, D, bs, P1, P2, d12, cap, uniq, ws, sr, mode),
+                nstripes=int(rng.choice([1, 3, 4, 8])), uniq_rule=int(rng.integers(0, 3)), seed=seed)
+
+
+CASES = [random_case(s) for s in range(36)]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"s{c['seed']}_{c['kind']}_m{c['args'][10]}" for c in CASES])
+def test_oracle_matches_volume_formulation(oracle, case):
+    L, R = S.adversarial_pair(case["kind"], case["H"], case["W"], case["args"][1], seed=case["seed"])
+    kw = dict(nstripes=case["nstripes"], uniq_rule=case["uniq_rule"])
+    for stages in (0, 3):  # after the LR check, and the full compute (median + speckle)
+        ref = oracle.sgbm_compute(L, R, oracle.make_params(*case["args"], **kw), stages=stages)
+        got = N.sgm_full_volume(L, R, *case["args"], stages=stages, **kw)
+        assert np.array_equal(ref, got), f"stages={stages}: {(ref != got).sum()} px differ"
+
+
+def test_volume_formulation_covers_saturation_and_ties(oracle):
+    """The adversarial set really reaches the edges it is meant to: a pixel whose every S
+    saturated (bestDisp stays -1), and exact first-minimum ties."""
+    L, R = S.adversarial_pair("binary", 19, 80, 48, seed=7)
+    args = (-3, 48, 11, 81, p2_domain_max(11, 63, 1), 1000000, 63, 5, 0, 0, 1)
+    e = N.sgm_effective(*args[:8], args[10])
+    ref = oracle.sgbm_compute(L, R, oracle.make_params(*args), stages=0)
+    assert np.array_equal(ref, N.sgm_full_volume(L, R, *args, stages=0))
+    pix = N.bt_cost_volume_rows(L, R, -3, 48, e["ftzero"]).astype(np.int64)
+    W1 = pix.shape[1]
+    xi = np.clip(np.arange(W1)[:, None] + np.arange(-5, 6)[None, :], 0, W1 - 1)
+    C = e["P2"] + N._box_rows(pix[:, xi, :].sum(2), 0, 19, 5, True)
+    Ssum = sum(N._path_volume(C, dx, dy, e["P1"], e["P2"]) for dx, dy in N.SGM_DIRS[1])
+    assert (np.minimum(Ssum, 32767).min(-1) == 32767).any()  # every d saturated somewhere
+    Lp, Rp = S.adversarial_pair("periodic", 12, 90, 32, seed=3)
+    args = (0, 32, 3, 8, 64, 1, 63, 0, 0, 0, 0)
+    ref = oracle.sgbm_compute(Lp, Rp, oracle.make_params(*args), stages=0)
+    assert np.array_equal(ref, N.sgm_full_volume(Lp, Rp, *args, stages=0))
+
+
+def test_int16_domain_bound_is_tight():
+    """At the engine's P2 bound the largest possible delta = minLp + P2 still fits a short."""
+    for bs in (1, 3, 5, 7, 9, 11):
+        for cap in (15, 63, 127):
+            ft = max(cap, 15) | 1
+            p2 = p2_domain_max(bs, cap, 0)
+            cmax = p2 + (2 * ft + 63) * bs * bs
+            assert cmax + p2 <= 32767 < cmax + p2 + 2

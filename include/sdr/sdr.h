@@ -264,6 +264,56 @@ int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float
 int sdr_pcd_header(int width, int height, char* buf, size_t cap);
 int sdr_write_pcd_binary(const char* path, const void* points, int width, int height);
 
+/* ---- display outputs: StereoDisparity::show_disparityMap / show_depthMap,
+ * the live loop's JET overlay and StereoDisplayer::depth_coverage ----
+ * Colour tables are 256 BGR triples (cv::applyColorMap's LUT); NULL = the built-in table of the
+ * colormap the reference uses (TURBO for the depth map, JET for the overlay), generated from the
+ * published colormap definitions by sdr_colormap_lut.  A display handle owns the EMA history
+ * (prev_vis / prev_depth_vis of stereo_disparity.hpp:11) and a default range state. */
+enum { SDR_COLORMAP_JET = 2, SDR_COLORMAP_TURBO = 20 }; /* cv::COLORMAP_* */
+typedef struct sdr_display sdr_display;
+int sdr_colormap_lut(int colormap, uint8_t* lut_bgr /* 768 bytes */);
+int sdr_display_create(int device, sdr_display** out);
+int sdr_display_destroy(sdr_display* h);
+int sdr_display_set_stream(sdr_display* h, void* stream); /* NULL = the HIP null stream */
+int sdr_display_reset_stream(sdr_display* h);              /* back to its own stream */
+/* forget the EMA history and reset the handle's range state to {1000, 2000} */
+int sdr_display_reset(sdr_display* h);
+/* show_disparityMap (stereo_disparity.cpp:42-73) on nframes float disparities (px; `stride` and
+ * `frame_stride` in ELEMENTS) -> d_vis u8 [F][H][W], frames in order through the EMA. */
+int sdr_show_disparity_map_device(sdr_display* h, const float* d_disp, int width, int height,
+                                  size_t stride, size_t frame_stride, int nframes,
+                                  int num_disparities, uint8_t* d_vis);
+/* show_depthMap (stereo_disparity.cpp:83-124) on computeDepth outputs (channels 3: Z is channel 2;
+ * channels 1: Z itself), dense [F][H][W][channels] -> d_bgr u8 [F][H][W][3].  d_zrange: device
+ * {zmin_smooth, zmax_smooth} (the reference's function-static doubles, shared by every caller
+ * that passes the same pointer), NULL = the handle's own.  coverage_pct (host [F], nullable):
+ * depth_coverage of each frame (stereo_displayer.cpp:105-118, columns >= 80); synchronises. */
+int sdr_show_depth_map_device(sdr_display* h, const float* d_xyz, int width, int height,
+                              int channels, int nframes, double* d_zrange, const uint8_t* lut_bgr,
+                              uint8_t* d_bgr, double* coverage_pct);
+/* StereoDisplayer::depth_coverage of xyz [F][H][W][3]: percent of Z in [0, 12000] among columns
+ * >= col0 (80 in the reference), over all H*W pixels (host pct[F]; synchronous). */
+int sdr_depth_coverage_device(sdr_display* h, const float* d_xyz, int width, int height,
+                              int nframes, int col0, double* pct);
+/* stereo_displayer.cpp:167-173: applyColorMap(vis, JET) -> d_heat (nullable) and
+ * addWeighted(resize(left_rect, 0.5, INTER_AREA), 0.7, heat, 0.3, 0) -> d_overlay (nullable), from
+ * the FULL-resolution rectified left BGR view (2*width x 2*height, left_stride bytes per row,
+ * left_frame_stride bytes per frame, 0 = dense); vis/heat/overlay are [F][H][W](x3). */
+int sdr_disparity_overlay_device(sdr_display* h, const uint8_t* d_vis, const uint8_t* d_left_bgr,
+                                 size_t left_stride, size_t left_frame_stride, int width,
+                                 int height, int nframes, const uint8_t* lut_bgr, uint8_t* d_heat,
+                                 uint8_t* d_overlay);
+/* Host-pointer versions (synchronous; `stride` in elements, out_stride in bytes).  zrange: host
+ * {zmin_smooth, zmax_smooth} in/out, NULL = the handle's own state. */
+int sdr_show_disparity_map(sdr_display* h, const float* disp, int width, int height, size_t stride,
+                           int num_disparities, uint8_t* out, size_t out_stride);
+int sdr_show_depth_map(sdr_display* h, const float* xyz, int width, int height, int channels,
+                       double* zrange, uint8_t* out_bgr, double* coverage_pct);
+int sdr_disparity_overlay(sdr_display* h, const uint8_t* vis, const uint8_t* left_bgr,
+                          size_t left_stride, int width, int height, uint8_t* heat,
+                          uint8_t* overlay);
+
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);
 

@@ -9,6 +9,8 @@
 //       stereo_disparity.cpp:10-13,31,36
 //   sdr::StereoDisparity                                     <- class StereoDisparity
 //       stereo_vision/include/stereo_disparity.hpp:8-24
+//   sdr::Display                                             <- show_disparityMap / show_depthMap,
+//       the displayer's JET overlay and depth_coverage (stereo_displayer.cpp:105-118,164-173)
 //
 // sdr::Mat is a minimal owning image (rows, cols, OpenCV type code, row step) so that callers
 // can switch from cv::Mat without OpenCV present; when OpenCV is available, wrap cv::Mat data
@@ -251,6 +253,60 @@ inline Ptr<DisparityWLSFilter> createDisparityWLSFilter(const Ptr<StereoSGBM>& l
 }
 }  // namespace ximgproc
 
+// Display outputs on the engine: the EMA history of one StereoDisparity
+// (prev_vis / prev_depth_vis, stereo_disparity.hpp:11), show_disparityMap / show_depthMap, the live
+// loop's JET overlay and StereoDisplayer::depth_coverage (stereo_displayer.cpp:105-118,167-173).
+class Display {
+public:
+    explicit Display(int device = 0) { check(sdr_display_create(device, &h_)); }
+    ~Display() { sdr_display_destroy(h_); }
+    Display(const Display&) = delete;
+    Display& operator=(const Display&) = delete;
+
+    // CV_32F disparity (px) -> CV_8UC1
+    Mat show_disparityMap(const Mat& disparity, int numDisparities) {
+        if (disparity.type != CV_32FC1) throw Exception(SDR_ERR_TYPE, "show_disparityMap expects CV_32F");
+        Mat out(disparity.rows, disparity.cols, CV_8UC1);
+        check(sdr_show_disparity_map(h_, disparity.ptr<float>(0), disparity.cols, disparity.rows,
+                                     disparity.step / 4, numDisparities, out.data, out.step));
+        return out;
+    }
+    // CV_32FC3 depth (Z = channel 2) or CV_32F Z -> CV_8UC3 (TURBO); zrange = {zmin, zmax} state
+    Mat show_depthMap(const Mat& depth, double* zrange, double* coverage_pct = nullptr) {
+        if (depth.type != CV_32FC3 && depth.type != CV_32FC1)
+            throw Exception(SDR_ERR_TYPE, "show_depthMap expects CV_32FC3 or CV_32F");
+        const int ch = depth.type == CV_32FC3 ? 3 : 1;
+        if (depth.step != (size_t)depth.cols * 4 * ch) throw Exception(SDR_ERR_ARG, "depth must be continuous");
+        Mat out(depth.rows, depth.cols, CV_8UC3);
+        check(sdr_show_depth_map(h_, depth.ptr<float>(0), depth.cols, depth.rows, ch, zrange, out.data,
+                                 coverage_pct));
+        return out;
+    }
+    // applyColorMap(vis, JET) + addWeighted(resize(left_rect, 0.5, INTER_AREA), 0.7, heat, 0.3, 0)
+    Mat overlay(const Mat& vis, const Mat& left_rect) {
+        if (vis.type != CV_8UC1 || left_rect.type != CV_8UC3 || left_rect.rows != 2 * vis.rows ||
+            left_rect.cols != 2 * vis.cols || vis.step != (size_t)vis.cols)
+            throw Exception(SDR_ERR_TYPE, "overlay expects CV_8UC1 vis and a CV_8UC3 left view of twice its size");
+        Mat out(vis.rows, vis.cols, CV_8UC3);
+        check(sdr_disparity_overlay(h_, vis.data, left_rect.data, left_rect.step, vis.cols, vis.rows,
+                                    nullptr, out.data));
+        return out;
+    }
+    // StereoDisplayer::depth_coverage(depth_map): percent of Z in [0, 12000] in columns >= 80
+    double depth_coverage(const Mat& depth) {
+        if (depth.type != CV_32FC3 || depth.step != (size_t)depth.cols * 12)
+            throw Exception(SDR_ERR_TYPE, "depth_coverage expects a continuous CV_32FC3 map");
+        Mat scratch(depth.rows, depth.cols, CV_8UC3);
+        double pct = 0, zr[2] = {1000.0, 2000.0};  // a throw-away range state: only the count is used
+        check(sdr_show_depth_map(h_, depth.ptr<float>(0), depth.cols, depth.rows, 3, zr, scratch.data, &pct));
+        return pct;
+    }
+    sdr_display* handle() const { return h_; }
+
+private:
+    sdr_display* h_ = nullptr;
+};
+
 // class StereoDisparity (reference stereo_vision/include/stereo_disparity.hpp:8-24)
 class StereoDisparity {
 public:
@@ -284,10 +340,26 @@ public:
     const Ptr<StereoSGBM> get_matcher() const { return matcher; }
     const Mat& getConfidenceMap() const { return conf_map; }  // wls_filter->getConfidenceMap() (:36)
 
+    // stereo_disparity.cpp:42-73: gamma map with the EMA against this object's previous frame
+    Mat show_disparityMap(const Mat& disparity) {
+        return display().show_disparityMap(disparity, matcher->getNumDisparities());
+    }
+    // stereo_disparity.cpp:83-124: the range state is function-static in the reference, i.e. one
+    // pair of doubles for every StereoDisparity of the process; so it is here
+    Mat show_depthMap(const Mat& depth) {
+        static double zrange[2] = {1000.0, 2000.0};
+        return display().show_depthMap(depth, zrange);
+    }
+
 private:
+    Display& display() {
+        if (!display_) display_ = std::make_shared<Display>(matcher->device());
+        return *display_;
+    }
     Ptr<StereoSGBM> matcher, right_matcher;
     Ptr<ximgproc::DisparityWLSFilter> wls_filter;
     Mat Q, conf_map;
+    Ptr<Display> display_;
 };
 
 }  // namespace sdr

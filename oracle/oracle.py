@@ -29,7 +29,8 @@ class OrcParams(ctypes.Structure):
 
 
 _SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "rectify_oracle.c",
-            "rectify_oracle.h", "pcl_oracle.c", "pcl_oracle.h", "Makefile")
+            "rectify_oracle.h", "pcl_oracle.c", "pcl_oracle.h", "display_oracle.c", "display_oracle.h",
+            "Makefile")
 
 
 def build(force: bool = False) -> str:
@@ -88,6 +89,16 @@ def lib():
                                      ctypes.POINTER(ci)]
         L.orc_voxel_grid.restype = ci
         L.orc_remap_bilinear_u8.argtypes = [u8p, ci, ci, sz, ci, i16p, u16p, ci, ci, u8p, sz]
+        L.orc_colormap_lut.argtypes = [ci, u8p]
+        L.orc_colormap_lut.restype = ci
+        L.orc_show_disparity_map.argtypes = [f32p, ci, ci, ci, u8p, u8p]
+        L.orc_depth_range_update.argtypes = [f32p, ci, ci, ci, f64p, f32p, f32p]
+        L.orc_show_depth_map.argtypes = [f32p, ci, ci, ci, f64p, u8p, u8p, u8p]
+        L.orc_apply_colormap.argtypes = [u8p, sz, u8p, u8p]
+        L.orc_add_weighted_u8.argtypes = [u8p, ctypes.c_double, u8p, ctypes.c_double, ctypes.c_double, sz, u8p]
+        L.orc_resize_area_half_bgr.argtypes = [u8p, ci, ci, sz, u8p]
+        L.orc_depth_coverage.argtypes = [f32p, ci, ci, ci]
+        L.orc_depth_coverage.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -319,3 +330,80 @@ def voxel_grid(points, leaf):
     flag = lib().orc_voxel_grid(_p(pts, ctypes.c_float), pts.shape[0], lx, ly, lz, _p(out, ctypes.c_float),
                                 ctypes.byref(cnt))
     return out[:cnt.value].copy(), bool(flag)
+
+
+# ---- display outputs (display_oracle.c) ----
+
+COLORMAP_JET, COLORMAP_TURBO = 2, 20
+
+
+def colormap_lut(colormap) -> np.ndarray:
+    out = np.empty((256, 3), np.uint8)
+    if lib().orc_colormap_lut(int(colormap), _p(out, ctypes.c_uint8)) != 0:
+        raise ValueError("unknown colormap")
+    return out
+
+
+def show_disparity_map(disp, num_disp, prev=None) -> np.ndarray:
+    d = np.ascontiguousarray(disp, np.float32)
+    h, w = d.shape
+    out = np.empty((h, w), np.uint8)
+    pv = None if prev is None else _p(np.ascontiguousarray(prev, np.uint8), ctypes.c_uint8)
+    lib().orc_show_disparity_map(_p(d, ctypes.c_float), w, h, int(num_disp), pv, _p(out, ctypes.c_uint8))
+    return out
+
+
+def show_depth_map(xyz, zrange, lut, prev=None) -> np.ndarray:
+    """zrange: float64 array [zmin_smooth, zmax_smooth], updated in place."""
+    x = np.ascontiguousarray(xyz, np.float32)
+    h, w = x.shape[:2]
+    ch = 1 if x.ndim == 2 else x.shape[2]
+    out = np.empty((h, w, 3), np.uint8)
+    lt = np.ascontiguousarray(lut, np.uint8)
+    pv = None if prev is None else _p(np.ascontiguousarray(prev, np.uint8), ctypes.c_uint8)
+    assert zrange.dtype == np.float64 and zrange.flags.c_contiguous
+    lib().orc_show_depth_map(_p(x, ctypes.c_float), w, h, ch, _p(zrange, ctypes.c_double),
+                             _p(lt, ctypes.c_uint8), pv, _p(out, ctypes.c_uint8))
+    return out
+
+
+def depth_range_update(xyz, zrange):
+    x = np.ascontiguousarray(xyz, np.float32)
+    h, w = x.shape[:2]
+    ch = 1 if x.ndim == 2 else x.shape[2]
+    a, b = ctypes.c_float(), ctypes.c_float()
+    lib().orc_depth_range_update(_p(x, ctypes.c_float), w, h, ch, _p(zrange, ctypes.c_double),
+                                 ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def apply_colormap(src, lut) -> np.ndarray:
+    s = np.ascontiguousarray(src, np.uint8)
+    out = np.empty(s.shape + (3,), np.uint8)
+    lt = np.ascontiguousarray(lut, np.uint8)
+    lib().orc_apply_colormap(_p(s, ctypes.c_uint8), s.size, _p(lt, ctypes.c_uint8), _p(out, ctypes.c_uint8))
+    return out
+
+
+def add_weighted(a, alpha, b, beta, gamma=0.0) -> np.ndarray:
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    assert a.shape == b.shape
+    out = np.empty_like(a)
+    lib().orc_add_weighted_u8(_p(a, ctypes.c_uint8), alpha, _p(b, ctypes.c_uint8), beta, gamma, a.size,
+                              _p(out, ctypes.c_uint8))
+    return out
+
+
+def resize_area_half_bgr(src) -> np.ndarray:
+    s = np.ascontiguousarray(src, np.uint8)
+    h, w, _ = s.shape
+    out = np.empty((h // 2, w // 2, 3), np.uint8)
+    lib().orc_resize_area_half_bgr(_p(s, ctypes.c_uint8), w, h, s.strides[0], _p(out, ctypes.c_uint8))
+    return out
+
+
+def depth_coverage(xyz, col0=80) -> float:
+    x = np.ascontiguousarray(xyz, np.float32)
+    h, w, _ = x.shape
+    return lib().orc_depth_coverage(_p(x, ctypes.c_float), w, h, int(col0))

@@ -8,6 +8,8 @@ from .sgbm import (  # noqa: F401
     cvt_bgr2gray, disparity_to_float, filterSpeckles, reprojectImageTo3D, resize_area_half,
 )
 from . import cloud  # noqa: F401
+from . import display  # noqa: F401
+from .display import COLORMAP_JET, COLORMAP_TURBO, Display, colormap_lut  # noqa: F401
 from .ximgproc import (  # noqa: F401
     DisparityWLSFilter, createDisparityWLSFilter, fastGlobalSmootherFilter,
 )
@@ -17,5 +19,6 @@ __all__ = [
     "SDRError", "SgbmParams", "StereoSGBM", "createRightMatcher", "reprojectImageTo3D",
     "disparity_to_float", "filterSpeckles", "cvt_bgr2gray", "resize_area_half",
     "MODE_SGBM", "MODE_HH", "MODE_SGBM_3WAY", "MODE_HH4", "WlsParams", "DisparityWLSFilter",
-    "createDisparityWLSFilter", "fastGlobalSmootherFilter", "StereoDisparity",
+    "createDisparityWLSFilter", "fastGlobalSmootherFilter", "StereoDisparity", "Display",
+    "colormap_lut", "COLORMAP_JET", "COLORMAP_TURBO",
 ]

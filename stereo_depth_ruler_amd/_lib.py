@@ -112,6 +112,19 @@ SIGNATURES = [
     ("sdr_write_pcd_binary", _i, [_c.c_char_p, _vp, _i, _i]),
     ("sdr_fgs_filter_device", _i, [_vp, _sz, _i, _i, _c.c_double, _c.c_double, _c.c_double, _i,
                                    _vp, _i, _vp]),
+    ("sdr_colormap_lut", _i, [_i, _vp]),
+    ("sdr_display_create", _i, [_i, _c.POINTER(_vp)]),
+    ("sdr_display_destroy", _i, [_vp]),
+    ("sdr_display_set_stream", _i, [_vp, _vp]),
+    ("sdr_display_reset_stream", _i, [_vp]),
+    ("sdr_display_reset", _i, [_vp]),
+    ("sdr_show_disparity_map_device", _i, [_vp, _vp, _i, _i, _sz, _sz, _i, _i, _vp]),
+    ("sdr_show_depth_map_device", _i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _c.POINTER(_c.c_double)]),
+    ("sdr_depth_coverage_device", _i, [_vp, _vp, _i, _i, _i, _i, _c.POINTER(_c.c_double)]),
+    ("sdr_disparity_overlay_device", _i, [_vp, _vp, _vp, _sz, _sz, _i, _i, _i, _vp, _vp, _vp]),
+    ("sdr_show_disparity_map", _i, [_vp, _vp, _i, _i, _sz, _i, _vp, _sz]),
+    ("sdr_show_depth_map", _i, [_vp, _vp, _i, _i, _i, _c.POINTER(_c.c_double), _vp, _c.POINTER(_c.c_double)]),
+    ("sdr_disparity_overlay", _i, [_vp, _vp, _vp, _sz, _i, _i, _vp, _vp]),
     ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),
     ("sdr_sgbm_enable_timing", _i, [_vp, _i]),
     ("sdr_sgbm_last_timing", _i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),

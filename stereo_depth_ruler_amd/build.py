@@ -14,7 +14,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libsdr.so")
 SOURCES = ["sdr_cost.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_rectify.hip",
-           "sdr_cloud.hip", "sdr_engine.hip"]
+           "sdr_cloud.hip", "sdr_display.hip", "sdr_engine.hip"]
 HEADERS = ["sdr_device.hpp", "sdr_internal.hpp"]
 ARCH = os.environ.get("SDR_OFFLOAD_ARCH", "gfx950")
 

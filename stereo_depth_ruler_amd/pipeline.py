@@ -1,8 +1,10 @@
 """Device pipelines for the reference's two per-frame loops, built from the engine's C ABI:
 
-* ``LiveLoop`` -- stereo_vision/src/stereo_displayer.cpp:145-162 (``show_disparity_overlay``):
+* ``LiveLoop`` -- stereo_vision/src/stereo_displayer.cpp:145-185 (``show_disparity_overlay``):
   side-by-side BGR frame -> split + StereoRectifier::rectify -> StereoDisparity::computeDisparity
-  (BGR2GRAY, INTER_AREA 0.5x, left 3WAY + right matcher, WLS, /16) -> computeDepth.
+  (BGR2GRAY, INTER_AREA 0.5x, left 3WAY + right matcher, WLS, /16) -> computeDepth, and with
+  ``display=True`` the loop's display outputs (show_depthMap, show_disparityMap, the JET overlay
+  on the half-size rectified left view; :164-173), frames of a batch in order through the EMAs.
 * ``CloudEmit`` -- point_cloud/src/pcd_write.cpp:81-130 (``save_and_display_pointcloud``):
   side-by-side BGR frame -> split -> BGR2GRAY -> StereoSGBM::compute -> /16 ->
   reprojectImageTo3D(handleMissing) -> convertCVMatToPCL(left) -> VoxelGrid.
@@ -18,6 +20,7 @@ import ctypes
 import numpy as np
 
 from ._lib import check, lib
+from .display import Display
 from .sgbm import MODE_SGBM_3WAY, StereoSGBM, _Q, createRightMatcher, torch
 from .ximgproc import createDisparityWLSFilter
 
@@ -29,7 +32,7 @@ def _vp(x):
 class LiveLoop:
     """The reference app's per-frame loop on one device (see module docstring)."""
 
-    def __init__(self, rectifier, Q, batch: int, device: int = 0, args=None):
+    def __init__(self, rectifier, Q, batch: int, device: int = 0, args=None, display: bool = False):
         self.rect = rectifier
         self.W, self.H = rectifier.W, rectifier.H
         self.Q = np.asarray(Q, np.float64)
@@ -49,6 +52,12 @@ class LiveLoop:
         self.disp = torch.empty((batch, h2, w2), dtype=torch.float32, **z)     # computeDisparity()
         self.filtered = torch.empty((batch, h2, w2), dtype=torch.int16, **z)
         self.depth = torch.empty((batch, h2, w2, 3), dtype=torch.float32, **z)  # computeDepth()
+        self.display = Display(device) if display else None
+        if display:
+            self.left_rect = torch.empty((batch, self.H, self.W, 3), dtype=torch.uint8, **z)
+            self.vis = torch.empty((batch, h2, w2), dtype=torch.uint8, **z)           # show_disparityMap
+            self.depth_vis = torch.empty((batch, h2, w2, 3), dtype=torch.uint8, **z)  # show_depthMap
+            self.overlay = torch.empty((batch, h2, w2, 3), dtype=torch.uint8, **z)    # overlay
 
     def matcher(self):
         return self.left
@@ -58,9 +67,10 @@ class LiveLoop:
         s = _vp(stream.cuda_stream)
         L = lib()
         check(L.sdr_rectifier_set_stream(self.rect._h, s))
+        disp_on = self.display is not None
         check(L.sdr_rectify_sbs_device(self.rect._h, sbs.data_ptr(), self.W * 6, self.W * 6 * self.H,
-                                       self.batch, None, None, self.small_l.data_ptr(),
-                                       self.small_r.data_ptr()))
+                                       self.batch, self.left_rect.data_ptr() if disp_on else None, None,
+                                       self.small_l.data_ptr(), self.small_r.data_ptr()))
         check(L.sdr_sgbm_set_stream(self.left._h, s))
         check(L.sdr_stereo_class_compute_device(self.left._h, self.right._h, self.wls._h,
                                                 self.small_l.data_ptr(), self.small_r.data_ptr(),
@@ -69,11 +79,22 @@ class LiveLoop:
         # computeDepth: reprojectImageTo3D(half-res disparity, full-res Q) (stereo_disparity.cpp:76-80)
         check(L.sdr_reproject_device(self.disp.data_ptr(), self.w2, self.h2, self.w2, _Q(self.Q), 0,
                                      self.depth.data_ptr(), self.w2 * 3, self.batch, s))
+        if disp_on:  # stereo_displayer.cpp:164-173
+            d, F, w2, h2 = self.display, self.batch, self.w2, self.h2
+            check(L.sdr_display_set_stream(d._h, s))
+            check(L.sdr_show_depth_map_device(d._h, self.depth.data_ptr(), w2, h2, 3, F, None, None,
+                                              self.depth_vis.data_ptr(), None))
+            check(L.sdr_show_disparity_map_device(d._h, self.disp.data_ptr(), w2, h2, w2, w2 * h2, F,
+                                                  self.left.getNumDisparities(), self.vis.data_ptr()))
+            check(L.sdr_disparity_overlay_device(d._h, self.vis.data_ptr(), self.left_rect.data_ptr(),
+                                                 self.W * 3, self.W * 3 * self.H, w2, h2, F, None, None,
+                                                 self.overlay.data_ptr()))
         return self.filtered
 
     def close(self):
-        for o in (self.left, self.right, self.wls):
-            o.close()
+        for o in (self.left, self.right, self.wls, self.display):
+            if o is not None:
+                o.close()
 
 
 class CloudEmit:

@@ -6,6 +6,9 @@ cvtColor(BGR2GRAY) -> resize(0.5, INTER_AREA) -> left SGBM (3WAY, d=80) and righ
 DisparityWLSFilter (lambda 8000, sigma 1.1) -> /16, all on the GPU (sdr_stereo_class_compute).
 computeDepth(disparity): reprojectImageTo3D(disparity, Q) (stereo_disparity.cpp:76-80), with the
 reference's quirk of a half-res disparity against the full-res Q kept as is.
+show_disparityMap / show_depthMap (stereo_disparity.cpp:42-73, 83-124): the display maps with their
+EMA state (prev_vis / prev_depth_vis per object; the depth-range smoothing state is shared by all
+objects, as the reference's function-static doubles are), on the GPU (csrc/sdr_display.hip).
 """
 from __future__ import annotations
 
@@ -14,12 +17,18 @@ import ctypes
 import numpy as np
 
 from ._lib import SDRError, check, lib
-from .sgbm import MODE_SGBM_3WAY, StereoSGBM, createRightMatcher, reprojectImageTo3D
+from .display import Display
+from .sgbm import MODE_SGBM_3WAY, StereoSGBM, _is_cuda, createRightMatcher, reprojectImageTo3D, torch
 from .ximgproc import createDisparityWLSFilter
 
 
 class StereoDisparity:
+    # show_depthMap's `static double zmin_smooth = 1000.0, zmax_smooth = 2000.0` (one per process)
+    _zrange_host = np.array([1000.0, 2000.0])
+    _zrange_dev = {}
+
     def __init__(self, Q_matrix, device: int = 0):
+        self._device = int(device)
         self.Q = np.asarray(Q_matrix, dtype=np.float64).reshape(4, 4).copy()
         # stereo_disparity.cpp:5-9
         self.matcher = StereoSGBM.create(0, 80, 5, 8 * 5 * 5 * 3, 32 * 5 * 5 * 3, 1, 63, 12, 200, 2,
@@ -33,6 +42,7 @@ class StereoDisparity:
         self.last_disp_right = None
         self.last_filtered = None
         self.conf_map = None
+        self._display = None
 
     def computeDisparity(self, left, right):
         left = np.ascontiguousarray(left, dtype=np.uint8)
@@ -59,3 +69,23 @@ class StereoDisparity:
 
     def get_matcher(self) -> StereoSGBM:
         return self.matcher
+
+    def _disp(self) -> Display:
+        if self._display is None:
+            self._display = Display(self._device)
+        return self._display
+
+    def show_disparityMap(self, disparity):
+        """stereo_disparity.cpp:42-73 (numDisparities read from the matcher, :43)."""
+        return self._disp().show_disparity_map(disparity, self.matcher.getNumDisparities())
+
+    def show_depthMap(self, depth):
+        """stereo_disparity.cpp:83-124 on computeDepth's output (or a Z map)."""
+        if _is_cuda(depth):
+            dev = depth.device.index
+            z = StereoDisparity._zrange_dev.get(dev)
+            if z is None:
+                z = torch.tensor([1000.0, 2000.0], dtype=torch.float64, device=depth.device)
+                StereoDisparity._zrange_dev[dev] = z
+            return self._disp().show_depth_map(depth, zrange=z)
+        return self._disp().show_depth_map(depth, zrange=StereoDisparity._zrange_host)

@@ -47,6 +47,18 @@ int main(int argc, char** argv) {
         dump(out + "/class_conf.bin", sd.getConfidenceMap());
         sdr::Mat depth = sd.computeDepth(df);
         dump(out + "/class_depth.bin", depth);
+        // display outputs (stereo_disparity.cpp:42-124, stereo_displayer.cpp:105-118,164-173): two
+        // frames each, so the second goes through the EMA against the first
+        for (int k = 0; k < 2; k++) {
+            sdr::Mat vis = sd.show_disparityMap(df), dv = sd.show_depthMap(depth);
+            dump(out + "/vis" + std::to_string(k) + ".bin", vis);
+            dump(out + "/depthvis" + std::to_string(k) + ".bin", dv);
+            if (k == 1) {
+                sdr::Display disp_out;
+                dump(out + "/overlay.bin", disp_out.overlay(vis, BL));
+                std::printf("coverage=%.17g\n", disp_out.depth_coverage(depth));
+            }
+        }
         std::printf("numDisparities=%d\n", sd.get_matcher()->getNumDisparities());
         // error behaviour: numDisparities not divisible by 16 -> exception, like cv::Exception
         try {

@@ -323,3 +323,20 @@ def test_cpp_facade(oracle, tmp_path):
     assert np.array_equal(cls, ref_cls)
     cconf = np.fromfile(tmp_path / "class_conf.bin", np.float32).reshape(H // 2, W // 2)
     assert np.array_equal(cconf.view(np.uint32), conf.view(np.uint32))
+    # display outputs through the facade, two frames (the second through the EMA)
+    h2, w2 = H // 2, W // 2
+    depth = oracle.reproject(ref_cls, S.REFERENCE_Q, False)
+    zr = np.array([1000.0, 2000.0])
+    turbo, jet = oracle.colormap_lut(oracle.COLORMAP_TURBO), oracle.colormap_lut(oracle.COLORMAP_JET)
+    pv = pd = None
+    for k in range(2):
+        vis = oracle.show_disparity_map(ref_cls, 80, pv)
+        dv = oracle.show_depth_map(depth, zr, turbo, pd)
+        assert np.array_equal(np.fromfile(tmp_path / f"vis{k}.bin", np.uint8).reshape(h2, w2), vis)
+        assert np.array_equal(np.fromfile(tmp_path / f"depthvis{k}.bin", np.uint8).reshape(h2, w2, 3), dv)
+        pv, pd = vis, dv
+    small = oracle.resize_area_half_bgr(bl)
+    ov = oracle.add_weighted(small, 0.7, oracle.apply_colormap(pv, jet), 0.3)
+    assert np.array_equal(np.fromfile(tmp_path / "overlay.bin", np.uint8).reshape(h2, w2, 3), ov)
+    cov = float(res.stdout.split("coverage=")[1].split()[0])
+    assert cov == oracle.depth_coverage(depth, 80)

@@ -201,3 +201,45 @@ def test_class_path_back_to_back_on_a_side_stream(cfg):
         assert torch.equal(rf, gf)
         assert torch.equal(ro.view(torch.int32), go.view(torch.int32))
     check(lib().sdr_sgbm_set_stream(left._h, ctypes.c_void_p(s0.cuda_stream)))
+
+
+def test_live_loop_with_display_outputs(oracle, cfg):
+    """pipeline.LiveLoop(display=True): the reference's whole per-frame loop body
+    (stereo_displayer.cpp:155-173) for a batch of 3 frames -- rectify, computeDisparity,
+    computeDepth, show_depthMap, show_disparityMap, JET overlay -- against the oracle chain,
+    frame by frame through the EMA state."""
+    from stereo_depth_ruler_amd.pipeline import LiveLoop
+
+    W, H = cfg.imageSize
+    F = 3
+    frames = sbs_frames(F, seed=31)
+    dev = torch.device("cuda", 0)
+    r = StereoRectifier(cfg)
+    loop = LiveLoop(r, cfg.Q, F, display=True)
+    loop.enqueue(torch.from_numpy(frames).to(dev), torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    ml, m2l = r.maps(0)
+    mr, m2r = r.maps(1)
+    turbo = oracle.colormap_lut(oracle.COLORMAP_TURBO)
+    jet = oracle.colormap_lut(oracle.COLORMAP_JET)
+    zr = np.array([1000.0, 2000.0])
+    pv = pd = None
+    h2, w2 = H // 2, W // 2
+    for f in range(F):
+        lrect = oracle.remap_bilinear(frames[f, :, :W], ml, m2l)
+        gl = oracle.resize_area_half(oracle.bgr2gray(lrect))
+        gr = oracle.resize_area_half(oracle.bgr2gray(oracle.remap_bilinear(frames[f, :, W:], mr, m2r)))
+        dl = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+        dr = oracle.sgbm_compute(gr, gl, oracle.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+        fd = oracle.wls_filter(dl, dr, gl, oracle.wls_params_for_sgbm(0, 80, 5, w2, h2, 8000.0, 1.1))
+        df = oracle.disp_to_float(fd)
+        depth = oracle.reproject(df, cfg.Q, False)
+        assert np.array_equal(loop.filtered[f].cpu().numpy(), fd)
+        assert np.array_equal(loop.left_rect[f].cpu().numpy(), lrect)
+        pd = oracle.show_depth_map(depth, zr, turbo, pd)
+        pv = oracle.show_disparity_map(df, 80, pv)
+        ov = oracle.add_weighted(oracle.resize_area_half_bgr(lrect), 0.7, oracle.apply_colormap(pv, jet), 0.3)
+        assert np.array_equal(loop.depth_vis[f].cpu().numpy(), pd)
+        assert np.array_equal(loop.vis[f].cpu().numpy(), pv)
+        assert np.array_equal(loop.overlay[f].cpu().numpy(), ov)
+    loop.close()

@@ -61,16 +61,37 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_cpu():
+    """(lscpu-style model name, logical CPUs this process may run on)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return model, n
+
+
 def cpu_baseline(cfg, seconds_target=15.0):
-    """The oracle (C restatement of the reference's OpenCV/ximgproc/PCL path) timed on host cores,
-    one frame per thread (ctypes releases the GIL), on a bounded sample of the same workload."""
+    """The oracle (C restatement of the reference's OpenCV/ximgproc/PCL path) timed on host cores
+    on a bounded sample of the same workload, two ways:
+      throughput -- one frame per thread, `threads` frames at a time (ctypes releases the GIL);
+      latency    -- one thread, one frame at a time (OpenCV's SGBM/HH run single-threaded).
+    threads = this GPU's share of the host: OMP_NUM_THREADS (16 per GPU on the GPU box, whose
+    nproc shows the whole machine), else every CPU the process may run on."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
     from stereo_depth_ruler_amd import synthetic as S
 
     _, W, H, args, _, hm, kind = cfg
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    model, ncpu = host_cpu()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(share, ncpu) if share > 0 else ncpu)
     p = O.make_params(*args)
     if kind == "sgbm":
         L, R, _ = S.make_pair(H, W, args[1], seed=12345)
@@ -114,6 +135,12 @@ def cpu_baseline(cfg, seconds_target=15.0):
             return 1
         what = (f"pcd_write frames (gray, {MODE_NAMES[args[10]]} d={args[1]}, reproject, cloud, VoxelGrid) from "
                 f"{2 * W}x{H} side-by-side BGR")
+    lat = []
+    for _ in range(3):  # latency: one thread, one frame
+        t = time.perf_counter()
+        one(0)
+        lat.append(time.perf_counter() - t)
+    lat_s = float(np.median(lat))
     frames = 0
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
@@ -126,7 +153,12 @@ def cpu_baseline(cfg, seconds_target=15.0):
         "cores": threads,
         "kind": "port",
         "sample": f"{frames} {what}, {threads} threads x 1 frame each, {el:.1f} s wall; oracle/*.c "
-                  f"(C restatement of OpenCV 4.6 / ximgproc / PCL; those libraries are absent on this image)",
+                  f"(a scalar C restatement of OpenCV 4.6 / ximgproc / PCL, not OpenCV itself, which is "
+                  f"absent on this image)",
+        "latency": {"ms_per_frame": round(lat_s * 1e3, 2), "value": round(W * H / lat_s / 1e6, 4),
+                    "unit": "Mpix/s", "threads": 1, "frames": len(lat)},
+        "host": {"cpu_model": model, "nproc": ncpu, "threads_used": threads,
+                 "omp_num_threads": share or None},
     }
 
 

@@ -339,7 +339,8 @@ int sdr_selftest_wave_ops(int* failures4);
  * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,
  * 2 = after the LR check, 3 = final (median + speckle), 4 = path costs L [P-1][F][H][W1][D] s16
  * (every direction but top-to-bottom, whose L is consumed on chip by the fused WTA pass),
- * 5 = disp2 keys of the fused WTA pass [F][H][W] u32 (minS << 16 | 0xffff - x). */
+ * 5 = the fused WTA pass's per-pixel (minS << 16 | bestDisp) [F][H][W] u32, indexed by matched
+ * column (0xffffffff: rejected); stage 1 holds values only in the matched columns. */
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
 
 const char* sdr_last_error(void);

@@ -8,9 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SDR_LIB_VARIANT selects an in-tree experiment build lib/libsdr-<variant>.so (scripts/exp_*.sh)
-_VARIANT = os.environ.get("SDR_LIB_VARIANT", "")
-LIB_PATH = os.path.join(_HERE, "lib", f"libsdr-{_VARIANT}.so" if _VARIANT else "libsdr.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libsdr.so")
 
 SDR_OK = 0
 ERRORS = {
@@ -48,6 +46,16 @@ class WlsParams(ctypes.Structure):
 
 
 _lib = None
+_path = LIB_PATH
+
+
+def use_library(path: str) -> None:
+    """Scripts only (experiment A/B, scripts/kbench.py): load `path` instead of lib/libsdr.so.
+    Must be called before the first use of the engine."""
+    global _path
+    if _lib is not None:
+        raise RuntimeError("the engine library is already loaded")
+    _path = os.path.abspath(path)
 
 # (name, restype, argtypes) for every function declared in include/sdr/sdr.h
 _c = ctypes
@@ -141,11 +149,11 @@ def lib():
     """Loads lib/libsdr.so (raises if the HIP extension has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if not os.path.exists(_path):
             raise RuntimeError(
-                f"HIP engine library missing: {LIB_PATH}. Build it with "
+                f"HIP engine library missing: {_path}. Build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950).")
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(_path)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)
             fn.restype = res

@@ -165,7 +165,7 @@ struct sdr_sgbm {
     std::vector<hipEvent_t> kev;
     std::vector<int> kkind;
     size_t kused = 0;
-    size_t path_slack = 0;  // elements of slack in front of C and Lr (last compute)
+    size_t path_slack = 0, path_lslack = 0;  // elements of slack in front of C / Lr (last compute)
     // class path: the right matcher runs on a side stream forked from / joined to this one
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -272,8 +272,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
     // the path kernels' loads overrun a chain's ends by up to kSouthPad rows: slack both sides
     const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
+    const size_t lslack = slack * (P - 1);
+    const size_t lfs = (size_t)(P - 1) * cells;  // L elements per frame, [H][W1][P-1][D]
     if ((rc = ensure(h->C, (F * cells + 2 * slack) * 2))) return rc;
-    if ((rc = ensure(h->Lr, ((size_t)(P - 1) * F * cells + 2 * slack) * 2))) return rc;
+    if ((rc = ensure(h->Lr, (F * lfs + 2 * lslack) * 2))) return rc;
     if ((rc = ensure(h->keys2, F * px * 4))) return rc;
     if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
     if ((rc = ensure(h->draw, F * px * 2))) return rc;
@@ -285,9 +287,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
 
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[0], st));
     h->path_slack = slack;
+    h->path_lslack = lslack;
     int16_t* C = (int16_t*)h->C.p + slack;
     int16_t* Caux = (int16_t*)h->Caux.p;
-    int16_t* Lr = (int16_t*)h->Lr.p + slack;  // [P-1][F][H][W1][D]
+    int16_t* Lr = (int16_t*)h->Lr.p + lslack;  // [F][H][W1][P-1][D]
     int16_t* draw = (int16_t*)h->draw.p;
     int16_t* dlr = (int16_t*)h->dlr.p;
 
@@ -333,6 +336,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     sdr::PathLaunch pls{}, plS{};
     pls.C = plS.C = C;
     pls.cs_fstride = plS.cs_fstride = cells;
+    pls.l_fstride = plS.l_fstride = lfs;
+    pls.l_pix = plS.l_pix = (P - 1) * g.D;
     pls.aux_fstride = plS.aux_fstride = aux_fstride;
     int nbuf = 0;
     auto add_dir = [&](sdr::PathLaunch& pl, int dir, int nch, int16_t* out) {
@@ -345,7 +350,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         d.out = out;
         pl.d[pl.ndirs++] = d;
     };
-    auto buf = [&]() { return Lr + (size_t)(nbuf++) * F * cells; };
+    auto buf = [&]() { return Lr + (size_t)(nbuf++) * g.D; };
     const int nE = H, nS = g.W1, nD = g.W1 + H - 1;
     // longest chains first: the E/W rows (W1 steps) are dispatched before the shorter ones
     add_dir(pls, sdr::DIR_E, nE, buf());
@@ -382,7 +387,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
     sdr::SouthWtaArgs wa{};
-    for (int p = 0; p < P - 1; p++) wa.L[p] = Lr + (size_t)p * F * cells;
+    wa.L = Lr;
     wa.npaths = P;
     wa.disp_raw = draw;
     wa.keys2 = (uint32_t*)h->keys2.p;
@@ -853,7 +858,8 @@ int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) 
     const Buf* b = stage == 0 ? &h->C : stage == 1 ? &h->draw : stage == 2 ? &h->dlr
                  : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : stage == 5 ? &h->keys2 : nullptr;
     if (!b) return fail(SDR_ERR_ARG, "bad stage");
-    const size_t skip = (stage == 0 || stage == 4) ? h->path_slack * 2 : 0;  // front slack
+    // front slack (the L records' is P-1 times C's)
+    const size_t skip = stage == 0 ? h->path_slack * 2 : stage == 4 ? h->path_lslack * 2 : 0;
     if (!b->p || bytes + skip > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));
     SDR_HIP(hipStreamSynchronize(h->stream));

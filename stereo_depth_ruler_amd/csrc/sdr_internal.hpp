@@ -39,7 +39,7 @@ struct Geometry {
 
 // ---- prefilter / cost volume (sdr_cost.hip) ----
 struct Planes {
-    uint64_t* L;        // [F][H][W] bytes {sob, sob_lo, sob_hi, raw, raw_lo, raw_hi, 0, 0}
+    uint64_t* L;        // [F][3][H][W] int16 splats: {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
     uint64_t* R;        // [F][3][H][W] int16 pairs (q(x) | q(x-1) << 16): {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
     size_t fstrideL, fstrideR;  // elements per frame
 };
@@ -67,12 +67,17 @@ struct PathDir {
     int ybeg, yend, write_from;  // DIR_S chain rows (3WAY stripes); others: 0, H, 0
     int aux_row0, aux_rows;      // DIR_S chains read stripe-local cost rows for their first rows
     const int16_t* Caux;         // [F][aux_rows][W1][D] or null
-    int16_t* out;                // L of this direction [F][H][W1][D]
+    int16_t* out;                // this direction's slot of the L records: L + dir_index * D
 };
 
+// The path costs of the P-1 directions k_paths writes are stored pixel-interleaved,
+// L[F][H][W1][P-1][D]: the fused WTA pass then reads one contiguous (P-1)*D record per pixel
+// instead of P-1 streams a whole volume apart.
 struct PathLaunch {
     const int16_t* C;
-    size_t cs_fstride;   // elements per frame (C and every L buffer)
+    size_t cs_fstride;   // elements per frame of C
+    size_t l_fstride;    // elements per frame of L
+    int l_pix;           // elements per pixel record of L ((P-1) * D)
     size_t aux_fstride;
     int ndirs;
     int prefix[kMaxPathDirs + 1];  // chain prefix sums
@@ -87,10 +92,10 @@ constexpr int kSouthIdx = 2;  // summation order E, W, S, SE, SW, N, NE, NW
 // clamped
 constexpr int kSouthPad = 64;
 struct SouthWtaArgs {
-    const int16_t* L[kMaxPaths];  // the P-1 other directions, in order, S removed
+    const int16_t* L;             // the P-1 other directions' records, in order, S removed
     int npaths;
-    int16_t* disp_raw;   // [F][H][W] WTA disparity (invalid outside the matched columns)
-    uint32_t* keys2;     // [F][H][W] disp2 keys (minS << 16 | 0xffff - x)
+    int16_t* disp_raw;   // [F][H][W] WTA disparity (written in the matched columns only)
+    uint32_t* keys2;     // [F][H][W] (minS << 16 | bestDisp) per matched column x (0xffffffff: rejected)
     size_t disp_fstride;
     int uniq, uniq_simd;
 };

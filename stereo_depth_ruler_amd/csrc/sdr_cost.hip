@@ -1,18 +1,20 @@
-// sdr_cost.hip -- A.1 prefilter + BT planes and A.2/A.3 cost volume kernels (CDNA4).
+// sdr_cost.hip -- A.1 prefilter + BT operands and A.2/A.3 cost volume kernels (CDNA4).
 //
-//   planes L  u64 [F][3][H][W]  int16 splats of the left image's BT operands at x:
-//                               {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}  (each 32-bit half = q|q<<16)
+//   L pack    u32 [F][H][W][3]  the left image's BT operands at x as 16-bit halves:
+//                               {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
 //   planes R  u64 [F][3][H][W]  int16 PAIRS of the right image's operands: q(x) | q(x-1) << 16, so a
 //                               lane holding disparities (d, d+1) reads one word for xr = x-d, x-d-1
 //   C         s16 [F][H][W1][D] P2 + blockSize^2 box sum of the BT pixel cost
 //
-// Cost kernel: lanes = disparity pairs (as in the path kernels), each wave walks CW output
-// columns; the horizontal window and the vertical running sum live in registers (static ring
-// slots by unrolling the row loop by the window height), the right image's pair planes for the
-// block's column span are staged in LDS (double-buffered, one barrier per row). The staged R
-// pair planes are split into even/odd-x halves: lane p reads entry x - 2p, so with the split
-// adjacent lanes read adjacent 8-byte words and ds_read_b64 is bank-conflict free (interleaved,
-// the -16 B lane stride hits each bank pair twice per 32-lane group).
+// Cost kernel: lanes = disparity pairs (as in the path kernels).  A block owns BCOLS output
+// columns and the BCOLS + 2*SW2 pixel-cost columns their windows need; each pixel cost is
+// computed once (the four waves own interleaved columns), summed vertically in registers (a ring
+// of the last NR rows, static slots by unrolling the row loop by the window height), and the
+// column sums are exchanged through LDS for the horizontal sums.  A pixel's left operands are
+// the same for all lanes: they are read from LDS as broadcasts and reach the packed ops through
+// op_sel half selection.  The right image's pair planes are staged per row (split into even/odd-x
+// halves so that lane p reading entry x - 2p is bank-conflict free), fetched two rows ahead
+// through registers and double-buffered in LDS.  One barrier per row.
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 
@@ -87,10 +89,17 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
             const uint32_t va = (uint32_t)(a >> (8 * c)) & 0xff, vb = (uint32_t)(b >> (8 * c)) & 0xff;
             w[c] = img ? (va | (vb << 16)) : va * 0x10001u;
         }
-        uint64_t* dst = (img ? pl.R + (size_t)f * pl.fstrideR : pl.L + (size_t)f * pl.fstrideL) + (size_t)y * W + x;
-        dst[0] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-        dst[plane] = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-        dst[2 * plane] = (uint64_t)w[4] | ((uint64_t)w[5] << 32);
+        if (img) {
+            uint64_t* dst = pl.R + (size_t)f * pl.fstrideR + (size_t)y * W + x;
+            dst[0] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            dst[plane] = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+            dst[2 * plane] = (uint64_t)w[4] | ((uint64_t)w[5] << 32);
+        } else {
+            uint32_t* dst = pl.L + (size_t)f * pl.fstrideL + ((size_t)y * W + x) * 3;
+            dst[0] = (w[0] & 0xffffu) | (w[1] << 16);
+            dst[1] = (w[2] & 0xffffu) | (w[3] << 16);
+            dst[2] = (w[4] & 0xffffu) | (w[5] << 16);
+        }
     }
 }
 
@@ -105,7 +114,9 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
 //   C(y, x, d) = P2 + sum_{|j|<=SH2} hsum(clamp(t(y)+j, s0, H-1), x, d),   t(y) = min(y, ylim)
 //   hsum(r, x, d) = sum_{|k|<=SW2} BT(r, clamp(x+k, 0, W1-1), d)
 // equals OpenCV's running sums in int16 wrap arithmetic, incl. the bottom rows where the running
-// sum stops updating (t clamps at ylim = H-1-SH2) and MODE_HH's untouched P2 rows.
+// sum stops updating (t clamps at ylim = H-1-SH2) and MODE_HH's untouched P2 rows.  The sums are
+// taken in the other order here, vertical first (V(x) = sum over the window's rows of BT(x)),
+// then horizontal over the V of the clamped columns: the same int16 wrap sum.
 // The window is walked over "virtual" rows q = t-SH2 .. t+SH2 (physical row clamp(q, s0, H-1)),
 // so the ring of the last NR rows is a plain sliding window with compile-time slots.
 // ------------------------------------------------------------------------------------------
@@ -113,11 +124,24 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
 // 32-lane staging store land on disjoint banks
 __host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 15) / 32 * 32 + 16; }
 
-template <int K>
+template <int NR, int K>
 struct CostCfg {
-    static constexpr int CW = K == 1 ? 8 : 4;  // output columns per wave
-    // waves per SIMD the register budget is capped for (the ring holds NR x K x CW pairs)
-    static constexpr int waves(int NR) { return NR * K <= 5 ? 3 : (NR * K <= 14 ? 2 : 1); }
+    static constexpr int SW2 = (NR - 1) / 2;
+    static constexpr int BCOLS = K == 1 ? 32 : 16;  // output columns of a block
+    static constexpr int CW = BCOLS / 4;            // output columns per wave (horizontal sums)
+    static constexpr int NPB = BCOLS + 2 * SW2;     // pixel-cost columns the block needs
+    static constexpr int PCW = (NPB + 3) / 4;       // pixel-cost columns per wave: p = wave + 4*jj
+    static constexpr int NLV = 4 * PCW;             // staged virtual columns
+    // row prefetch depth and the row loop's unroll: U covers the ring slot (% NR), the LDS
+    // double buffer (% 2) and the prefetch register slot (% PD) statically
+    // (two rows: deeper prefetch costs registers, i.e. resident blocks, and measured slower)
+    static constexpr int PD = 2;
+    static constexpr int U = 2 * NR;
+    // LDS bytes: two staging buffers (R: 3 pair planes x 2 parity halves, L: 4 words a column)
+    // + two column-sum buffers
+    static size_t lds_bytes(int D) {
+        return (size_t)2 * 6 * cost_half_r(NLV + D) * 8 + (size_t)2 * NLV * 16 + (size_t)2 * NLV * K * 64 * 4;
+    }
 };
 
 // Birchfield-Tomasi dissimilarity of packed pairs: min(max(0, u-v1, v0-u), max(0, v-u1, u0-v)).
@@ -129,231 +153,259 @@ __device__ __forceinline__ uint32_t bt_cost(uint32_t u, uint32_t u0, uint32_t u1
     const uint32_t c1 = pk_max_u(pk_sub_usat(v, u1), pk_sub_usat(u0, v));
     return pk_min_u(c0, c1);
 }
-
-// pix[j] = pix[src] for the columns a block-edge wave sees beyond the image (x clamped to
-// [0, W1-1]): J0 = first in-image column (left edge), J1 = last in-image column (right edge)
-template <int K, int NC, int J0>
-__device__ __forceinline__ void clamp_left(uint32_t (&pix)[K][NC]) {
-#pragma unroll
-    for (int i = 0; i < K; i++)
-#pragma unroll
-        for (int j = 0; j < J0; j++) pix[i][j] = pix[i][J0];
+// a 16-bit half of a word broadcast to both halves: folds into the packed op as an op_sel
+// operand selection
+__device__ __forceinline__ uint32_t half_lo(uint32_t w) {
+    const u16x2 v = as_u16x2(w);
+    return as_u32(__builtin_shufflevector(v, v, 0, 0));
 }
-template <int K, int NC, int J1>
-__device__ __forceinline__ void clamp_right(uint32_t (&pix)[K][NC]) {
-#pragma unroll
-    for (int i = 0; i < K; i++)
-#pragma unroll
-        for (int j = J1 + 1; j < NC; j++) pix[i][j] = pix[i][J1];
-}
-template <int K, int NC, int... J>
-__device__ __forceinline__ void clamp_edges(uint32_t (&pix)[K][NC], int j0, int j1,
-                                            std::integer_sequence<int, J...>) {
-    ((j0 == J ? clamp_left<K, NC, J>(pix) : void()), ...);
-    ((j1 == J ? clamp_right<K, NC, J>(pix) : void()), ...);
+__device__ __forceinline__ uint32_t half_hi(uint32_t w) {
+    const u16x2 v = as_u16x2(w);
+    return as_u32(__builtin_shufflevector(v, v, 1, 1));
 }
 
-template <int NR, int K>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CostCfg<K>::waves(NR)))) void k_cost(Geometry g, CostArgs a) {
-    constexpr int SW2 = (NR - 1) / 2, SH2 = SW2;
-    constexpr int CW = CostCfg<K>::CW;
-    constexpr int NC = CW + 2 * SW2;
-    constexpr int BCOLS = 4 * CW;
-    constexpr int NLV = BCOLS + 2 * SW2;  // staged (virtual) columns of a block
-    extern __shared__ uint64_t lds[];
+template <int NR, int K, bool EDGE>
+__device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a, uint64_t* lds,
+                                           int bx, int f, int ty0, int ty1) {
+    using Cfg = CostCfg<NR, K>;
+    constexpr int SW2 = Cfg::SW2, SH2 = SW2, BCOLS = Cfg::BCOLS, CW = Cfg::CW;
+    constexpr int PCW = Cfg::PCW, NLV = Cfg::NLV, PD = Cfg::PD, U = Cfg::U;
+    static_assert(U % PD == 0 && U % NR == 0 && U % 2 == 0, "static slots");
     const int W = g.W, H = g.H, W1 = g.W1, D = g.D;
     const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int f = blockIdx.z;
-    const int bx0 = blockIdx.x * BCOLS;
-    const int wx0 = bx0 + wave * CW;
-    const int ty0 = a.row_begin + blockIdx.y * a.TY;
-    const int ty1 = min(ty0 + a.TY, a.row_end);
-    if (ty0 >= ty1) return;
+    const int bx0 = bx * BCOLS;
     const uint32_t P2x2 = splat16(g.P2);
     int16_t* out = a.out + (size_t)f * a.out_fstride;
 
-    // output addressing: uniform row base + per-lane byte offset; the wave's column count and
-    // the active-lane predicate are hoisted so each row is one exec region of plain stores
-    const int ncols = min(CW, W1 - wx0);
-    const size_t colstride = (size_t)D * 2;
-    auto row_base = [&](int y) {
-        return (char*)(out + ((size_t)(y - a.out_row0) * W1 + wx0) * D) + 4 * lane;
-    };
-    auto emit = [&](int y, auto&& val) __attribute__((always_inline)) {
-        char* rb = row_base(y);
+    // output addressing: the wave's first row and column in a buffer resource, rows and columns
+    // as scalar offsets, the lane's pair as the one vector offset.  Lanes past the last
+    // disparity pair alias it (they compute and store the same value to the same word), so every
+    // store is unconditional and the number of stores per row is static: hipcc then counts the
+    // outstanding stores exactly and does not wait for the row prefetches behind them.
+    const int ox0 = bx0 + wave * CW;
+    const int ncols = EDGE ? min(CW, W1 - ox0) : CW;
+    const uint32_t colb = (uint32_t)D * 2, rowb = (uint32_t)W1 * colb;
+    const Rsrc rO = rsrc_at(out + ((size_t)(ty0 - a.out_row0) * W1 + ox0) * D);
+    const Rsrc rSink = rsrc_at(a.sink + (size_t)ox0 * D);
+    int qpc[K];
+    uint32_t vo[K];
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-            if (2 * (lane + 64 * i) < D) {
+    for (int i = 0; i < K; i++) {
+        qpc[i] = min(lane + 64 * i, D / 2 - 1);
+        vo[i] = 4 * qpc[i];
+    }
+    auto emit_at = [&](Rsrc r, uint32_t so, auto&& val) __attribute__((always_inline)) {
 #pragma unroll
-                for (int c = 0; c < CW; c++)
-                    if (c < ncols) *(uint32_t*)(rb + c * colstride + 256 * i) = val(i, c);
-            }
-        }
+        for (int i = 0; i < K; i++)
+#pragma unroll
+            for (int c = 0; c < CW; c++)
+                if (!EDGE || c < ncols) __builtin_amdgcn_raw_buffer_store_b32(val(i, c), r, vo[i], so + c * colb, 0);
     };
+    auto emit = [&](int y, auto&& val) __attribute__((always_inline)) { emit_at(rO, (uint32_t)(y - ty0) * rowb, val); };
 
     // rows [yl, ty1) of MODE_HH keep the initial P2
     int yl = ty1;
     if (a.hh_bottom) yl = max(ty0, min(ty1, max(1, H - SH2)));
-    auto emit_p2 = [&](int y) { emit(y, [&](int, int) { return P2x2; }); };
-    for (int y = yl; y < ty1; y++) emit_p2(y);
+    for (int y = yl; y < ty1; y++) emit(y, [&](int, int) { return P2x2; });
     if (yl <= ty0) return;
 
-    // Staged spans in VIRTUAL columns v = bx0 - SW2 + e (e = 0 .. NLV-1): L at image column
-    // minX1 + clamp(v); R pairs for xr = minX1 + v - minD - (D-2) + e', e' = 0 .. NLV+D-3, the
-    // right image's pair of disparities (2qp, 2qp+1) of column v at e' = (v - vlo) + D-2 - 2qp.
-    // Sources are clamped into the image; columns a wave sees beyond [0, W1) are then replaced
-    // by the edge column's pixel cost (clamp_edges), which is what x clamping means.
+    // Virtual columns v = vlo + p, p = 0 .. NLV-1; wave w computes the pixel costs of columns
+    // p = w + 4*jj.  Left operands are staged for image columns minX1 + clamp(v, 0, W1-1); R pairs
+    // for xr = minX1 + vlo - minD - (D-2) + e, e = 0 .. NLV+D-3: the pair of disparities
+    // (2qp, 2qp+1) of column p sits at e = p + D-2 - 2qp.  Columns beyond [0, W1) are computed
+    // from clamped data and never read: the horizontal sums read the column sums of clamp(v),
+    // which is what x clamping means.
     const int vlo = bx0 - SW2;
     const int NRP = NLV + D - 2;
-    const int STR = BCOLS + 2 * SW2 + D;
-    const int HR = cost_half_r(STR);  // entries per parity half of a staged R plane
-    const int BUF = 3 * STR + 6 * HR;
-    const uint64_t* PLf = a.pl.L + (size_t)f * a.pl.fstrideL;
-    const uint64_t* PRf = a.pl.R + (size_t)f * a.pl.fstrideR;
-    const size_t plane = (size_t)H * W;
+    const int HR = cost_half_r(NLV + D);  // entries per parity half of a staged R plane
+    const int BUFR = 6 * HR;
+    uint32_t* LB = (uint32_t*)(lds + 2 * BUFR);  // [2][NLV][4] left operand words
+    uint32_t* VB = LB + 2 * NLV * 4;             // [2][NLV][K][64] column sums
+    const uint32_t planeb = (uint32_t)H * W * 8;
 
-    // ---- staging: rows of the L splat planes and R pair planes into LDS buffer b ----
-    // Loads are unconditional with clamped indices (surplus lanes re-load and re-store the last
-    // entry, the same value to the same slot): a guarded load makes hipcc branch around it and
-    // wait vmcnt(0) right after the prefetch is issued, exposing the full HBM latency per row.
+    // ---- staging: a row of the R pair planes and of the L pack, global -> registers -> LDS ----
+    // Rows are fetched PD rows ahead into PD register slots (slot of row r: (r - qbeg) % PD), so
+    // a load has PD row steps to land.  Loads are unconditional with clamped indices and
+    // rows (surplus lanes re-load and re-store the last entry, the same value to the same slot):
+    // a guarded load makes hipcc branch around it and wait vmcnt(0) right after it is issued.
+    // Staging goes through registers, not LDS-direct loads, because the barrier of every row
+    // would then wait for all of them.
     constexpr int NPR = K;  // R entries per thread per plane: NRP <= 256 * K
-    const int il = min(tid, NLV - 1);
-    const int gl = g.minX1 + min(max(vlo + il, 0), W1 - 1);
     const int xr0 = g.minX1 + vlo - g.minD - (D - 2);
-    int gr[NPR], pr[NPR];
+    const Rsrc rR = rsrc_at(a.pl.R + (size_t)f * a.pl.fstrideR);  // < 2 GiB a frame (check_frame)
+    const Rsrc rL = rsrc_at(a.pl.L + (size_t)f * a.pl.fstrideL);
+    uint32_t gr[NPR];
+    int pr[NPR];
 #pragma unroll
     for (int t = 0; t < NPR; t++) {
         const int ir = min(tid + 256 * t, NRP - 1);
-        gr[t] = min(max(xr0 + ir, 0), W - 1);
+        gr[t] = 8 * min(max(xr0 + ir, 0), W - 1);
         pr[t] = (ir & 1) * HR + (ir >> 1);
     }
-    uint64_t ql[3], qr[3][NPR];
-    auto fetch = [&](int r) {
-        const uint64_t* prow = PLf + (size_t)r * W;
-        const uint64_t* rrow = PRf + (size_t)r * W;
-#pragma unroll
-        for (int k = 0; k < 3; k++) ql[k] = prow[k * plane + gl];
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-#pragma unroll
-            for (int t = 0; t < NPR; t++) qr[k][t] = rrow[k * plane + gr[t]];
+    const int il = min(tid, 3 * NLV - 1);  // L word il: column il / 3, word il % 3
+    const uint32_t gl = 4 * (3 * (g.minX1 + min(max(vlo + il / 3, 0), W1 - 1)) + il % 3);
+    const int pl = (il / 3) * 4 + il % 3;
+    struct Stage {
+        uint64_t r[3][NPR];
+        uint32_t l;
     };
-    auto put = [&](int b) {
-        uint64_t* B = lds + (size_t)b * BUF;
-        uint64_t* BR = B + 3 * STR;
-#pragma unroll
-        for (int k = 0; k < 3; k++) B[k * STR + il] = ql[k];
+    Stage st[PD];
+    auto fetch = [&](int r, Stage& sg) __attribute__((always_inline)) {
+        const uint32_t so = (uint32_t)r * W * 8;
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
-            for (int t = 0; t < NPR; t++) BR[k * 2 * HR + pr[t]] = qr[k][t];
+            for (int t = 0; t < NPR; t++) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rR, gr[t], so + k * planeb, 0);
+                sg.r[k][t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+            }
+        sg.l = __builtin_amdgcn_raw_buffer_load_b32(rL, gl, (uint32_t)r * W * 12, 0);
+    };
+    auto put = [&](int b, const Stage& sg) __attribute__((always_inline)) {
+        uint64_t* BR = lds + b * BUFR;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+#pragma unroll
+            for (int t = 0; t < NPR; t++) BR[k * 2 * HR + pr[t]] = sg.r[k][t];
+        LB[b * NLV * 4 + pl] = sg.l;
     };
 
-    // per-lane staged R position of column j: (j & 1) * HR + (wave*CW + j) / 2 + (D-2)/2 - qp
+    // per-lane staged R position of this wave's column jj: (p & 1) * HR + p / 2 + (D-2)/2 - qp
+    // with p = wave + 4*jj, i.e. rpos + 2*jj
     int rpos[K];
-    bool act[K];
 #pragma unroll
-    for (int i = 0; i < K; i++) {
-        const int qp = lane + 64 * i;
-        act[i] = 2 * qp < D;
-        rpos[i] = 3 * STR + wave * (CW / 2) + (act[i] ? (D - 2) / 2 - qp : 0);
-    }
-    const int lpos = wave * CW;
-    // block-edge waves: first / last in-image column among the wave's NC (NC = none)
-    const int j0 = max(0, -(wx0 - SW2));
-    const int j1 = min(NC - 1, W1 - 1 - (wx0 - SW2));
-    const bool edge = (j0 > 0) | (j1 < NC - 1);
+    for (int i = 0; i < K; i++) rpos[i] = (wave & 1) * HR + (wave >> 1) + (D - 2) / 2 - qpc[i];
+    // column sums: written at [p][i][lane], read back for columns clamp(wave*CW + c', plo, phi)
+    uint32_t* Vw = VB + (wave * K) * 64 + lane;
+    const int plo = SW2 - bx0, phi = W1 - 1 - vlo;
 
     // virtual rows and outputs
     const int ylim = a.ylim, s0 = a.s0;
     const int tfirst = min(ty0, ylim), tlast = min(yl - 1, ylim);
     const int qbeg = tfirst - SH2, qend = tlast + SH2;
-    auto phys = [&](int q) { return min(max(q, s0), H - 1); };
+    auto phys = [&](int q) { return min(max(min(q, qend), s0), H - 1); };
 
-    uint32_t ring[NR][K][CW], sum[K][CW];
+    // horizontal sums (+ P2) of the column sums in buffer b
+    auto hsum = [&](int b, uint32_t (&hs)[K][CW]) __attribute__((always_inline)) {
+        const uint32_t* V = VB + b * (NLV * K * 64) + (wave * CW) * K * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < K; i++) {
+            uint32_t v[CW + 2 * SW2];
+#pragma unroll
+            for (int c = 0; c < CW + 2 * SW2; c++) {
+                int dc = c;  // interior: immediate offsets from one base
+                if (EDGE) dc = min(max(wave * CW + c, plo), phi) - wave * CW;
+                v[c] = V[(dc * K + i) * 64];
+            }
+            uint32_t h = P2x2;
+#pragma unroll
+            for (int k = 0; k < 2 * SW2 + 1; k++) h = pk_add(h, v[k]);
+            hs[i][0] = h;
+#pragma unroll
+            for (int c = 1; c < CW; c++) {
+                h = pk_sub(pk_add(h, v[c + 2 * SW2]), v[c - 1]);
+                hs[i][c] = h;
+            }
+        }
+    };
+
+    uint32_t ring[NR][K][PCW], vs[K][PCW];
 #pragma unroll
     for (int s = 0; s < NR; s++)
 #pragma unroll
         for (int i = 0; i < K; i++)
 #pragma unroll
-            for (int c = 0; c < CW; c++) ring[s][i][c] = 0;
+            for (int jj = 0; jj < PCW; jj++) ring[s][i][jj] = 0;
 #pragma unroll
     for (int i = 0; i < K; i++)
 #pragma unroll
-        for (int c = 0; c < CW; c++) sum[i][c] = 0;
+        for (int jj = 0; jj < PCW; jj++) vs[i][jj] = 0;
 
-    fetch(phys(qbeg));
-    put(0);
-    if (qbeg + 1 <= qend) fetch(phys(qbeg + 1));
+    fetch(phys(qbeg), st[0]);
+    put(0, st[0]);
+#pragma unroll
+    for (int k = 1; k <= PD; k++) fetch(phys(qbeg + k), st[k % PD]);
     __syncthreads();
 
-    auto row = [&](const int q, auto sc) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        const int b = (q - qbeg) & 1;
-        if (q + 1 <= qend) {
-            put(b ^ 1);
-            if (q + 2 <= qend) fetch(phys(q + 2));
+    // one barrier per virtual row q = qbeg + j (mod U): (A) horizontal sums + outputs of the
+    // column sums row q-1 left in LDS, (B) staging of row q+1 and the fetch of row q+1+PD, (C)
+    // pixel costs of row q, the vertical window, its column sums into LDS
+    auto row = [&](const int q, auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int s = j % NR, b = j & 1;
+        {
+            // output row t = q-1-SH2 < tlast; rows before ty0 (the window's warm-up, or a band in
+            // the frozen bottom rows) go to the sink row instead of a branch around the stores
+            uint32_t hs[K][CW];
+            hsum(b ^ 1, hs);
+            const int t = q - 1 - SH2;
+            const bool real = t >= ty0;
+            emit_at(real ? rO : rSink, real ? (uint32_t)(t - ty0) * rowb : 0u, [&](int i, int c) { return hs[i][c]; });
         }
-        const uint64_t* B = lds + (size_t)b * BUF;
-        const uint64_t* BL = B + lpos;
-        // pixel costs of the NC columns of this wave, then the horizontal window sums
-        uint32_t hs[K][CW];
-        uint32_t pix[K][NC];
+        put((j + 1) & 1, st[(j + 1) % PD]);
+        fetch(phys(q + 1 + PD), st[(j + 1) % PD]);
+        const uint64_t* BR = lds + b * BUFR;
+        const uint32_t* BL = LB + b * NLV * 4 + wave * 4;
 #pragma unroll
-        for (int j = 0; j < NC; j++) {
-            // broadcast LDS reads (every lane the same address) of the L operands
-            const uint64_t l0 = BL[j], l1 = BL[STR + j], l2 = BL[2 * STR + j];
-            const uint32_t u = (uint32_t)l0, u0 = (uint32_t)(l0 >> 32), u1 = (uint32_t)l1;
-            const uint32_t ur = (uint32_t)(l1 >> 32), ur0 = (uint32_t)l2, ur1 = (uint32_t)(l2 >> 32);
+        for (int jj = 0; jj < PCW; jj++) {
+            // a broadcast read: every lane reads the column's three words
+            const uint32_t w0 = BL[16 * jj], w1 = BL[16 * jj + 1], w2 = BL[16 * jj + 2];
+            const uint32_t u = half_lo(w0), u0 = half_hi(w0), u1 = half_lo(w1);
+            const uint32_t ur = half_hi(w1), ur0 = half_lo(w2), ur1 = half_hi(w2);
 #pragma unroll
             for (int i = 0; i < K; i++) {
-                const uint64_t* BRj = B + rpos[i] + (j & 1) * HR + (j >> 1);
+                const uint64_t* BRj = BR + rpos[i] + 2 * jj;
                 const uint64_t r0 = BRj[0], r1 = BRj[2 * HR], r2 = BRj[4 * HR];
                 const uint32_t bs = bt_cost(u, u0, u1, (uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1);
                 const uint32_t br = bt_cost(ur, ur0, ur1, (uint32_t)(r1 >> 32), (uint32_t)r2, (uint32_t)(r2 >> 32));
-                pix[i][j] = pk_add(bs, pk_shr2_u(br));
+                const uint32_t pix = pk_add(bs, pk_shr2_u(br));
+                vs[i][jj] = pk_sub(pk_add(vs[i][jj], pix), ring[s][i][jj]);
+                ring[s][i][jj] = pix;
             }
         }
-        if (edge) clamp_edges(pix, j0, j1, std::make_integer_sequence<int, NC>{});
+        {
+            // (partial sums during the warm-up: their horizontal sums go to the sink)
+            uint32_t* Vb = Vw + b * (NLV * K * 64);
 #pragma unroll
-        for (int i = 0; i < K; i++) {
-            uint32_t h = 0;
+            for (int jj = 0; jj < PCW; jj++)
 #pragma unroll
-            for (int k = 0; k < 2 * SW2 + 1; k++) h = pk_add(h, pix[i][k]);
-            hs[i][0] = h;
-#pragma unroll
-            for (int c = 1; c < CW; c++) {
-                h = pk_sub(pk_add(h, pix[i][c + 2 * SW2]), pix[i][c - 1]);
-                hs[i][c] = h;
-            }
-#pragma unroll
-            for (int c = 0; c < CW; c++) {
-                sum[i][c] = pk_sub(pk_add(sum[i][c], hs[i][c]), ring[s][i][c]);
-                ring[s][i][c] = hs[i][c];
-            }
-        }
-        // emit the output rows centred on t = q - SH2 once the window is full
-        if (q - qbeg >= NR - 1) {
-            const int t = q - SH2;
-            const int ya = (t == tlast) ? max(t, ty0) : t;
-            const int yb = (t == tlast) ? yl : t + 1;
-            for (int y = ya; y < yb; y++) emit(y, [&](int i, int c) { return pk_add(sum[i][c], P2x2); });
+                for (int i = 0; i < K; i++) Vb[(4 * jj * K + i) * 64] = vs[i][jj];
         }
         __syncthreads();
     };
     int qq = qbeg;
-    for (; qq + NR - 1 <= qend; qq += NR) unroll_rows(row, qq, std::make_integer_sequence<int, NR>{});
-    unroll_rows_tail(row, qq, qend, std::make_integer_sequence<int, NR>{});
+    for (; qq + U - 1 <= qend; qq += U) unroll_rows(row, qq, std::make_integer_sequence<int, U>{});
+    unroll_rows_tail(row, qq, qend, std::make_integer_sequence<int, U>{});
+    // the last window, t = tlast: its rows [max(tlast, ty0), yl) (the frozen bottom rows repeat it)
+    uint32_t hs[K][CW];
+    hsum((qend - qbeg) & 1, hs);
+    for (int y = max(tlast, ty0); y < yl; y++) emit(y, [&](int i, int c) { return hs[i][c]; });
+}
+
+template <int NR, int K>
+__global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
+    using Cfg = CostCfg<NR, K>;
+    extern __shared__ uint64_t lds[];
+    // column blocks of one row band are consecutive logical blocks: they share an XCD, so the
+    // right-image rows they all stage (each block reads D-2 columns of halo) are re-read from L2
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int l = xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
+    const int bx = l % gx, by = (l / gx) % gy, f = l / (gx * gy);
+    const int ty0 = a.row_begin + by * a.TY;
+    const int ty1 = min(ty0 + a.TY, a.row_end);
+    if (ty0 >= ty1) return;
+    const int bx0 = bx * Cfg::BCOLS;
+    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, true>(g, a, lds, bx, f, ty0, ty1);
+    else cost_block<NR, K, false>(g, a, lds, bx, f, ty0, ty1);
 }
 
 template <int NR, int K>
 static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) {
-    constexpr int BCOLS = 4 * CostCfg<K>::CW;
+    using Cfg = CostCfg<NR, K>;
     const int rows = a.row_end - a.row_begin;
-    const int STR = BCOLS + 2 * ((NR - 1) / 2) + g.D;
-    const size_t lds = (size_t)2 * (3 * STR + 6 * cost_half_r(STR)) * 8;
-    const int colblocks = (g.W1 + BCOLS - 1) / BCOLS;
+    const size_t lds = Cfg::lds_bytes(g.D);
+    const int colblocks = (g.W1 + Cfg::BCOLS - 1) / Cfg::BCOLS;
     if (a.TY <= 0) {
         // one full pass of resident blocks: a partial second pass doubles the kernel time, and
         // each block re-walks NR-1 warm-up rows, so use the tallest row band that fills the chip
@@ -373,6 +425,9 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
     dim3 grid(colblocks, (rows + a.TY - 1) / a.TY, F);
     hipLaunchKernelGGL((k_cost<NR, K>), grid, dim3(256), lds, st, g, a);
 }
+
+// one output row of the widest column-block span (racing garbage from every block)
+size_t cost_sink_bytes(const Geometry& g) { return (size_t)(g.W1 + 64) * g.D * 2; }
 
 bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.SH2 <= 5 && g.D <= 256; }
 

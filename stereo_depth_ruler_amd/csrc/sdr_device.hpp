@@ -139,7 +139,67 @@ __device__ __forceinline__ uint32_t row16_min_u32(uint32_t m) {
     return min_u32_dpp<kDppRowMirror>(m);
 }
 
+template <int K>
+struct Regs {
+    uint32_t r[K];
+};
+
+// Buffer-resource access: the row base lives in a wave-uniform resource descriptor (SGPRs, scalar
+// arithmetic), the lane's byte offset in one VGPR, so a load or store costs no vector address math.
+using Rsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ Rsrc rsrc_at(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// K packed pairs at the lane's byte offset vofs plus a wave-uniform (SGPR) byte offset sofs: one
+// resource per buffer for a whole chain, and one scalar add per step moves every access of the step
+template <int K>
+__device__ __forceinline__ Regs<K> load_buf(Rsrc r, uint32_t vofs, uint32_t sofs = 0) {
+    Regs<K> v;
+    if constexpr (K == 1) {
+        v.r[0] = __builtin_amdgcn_raw_buffer_load_b32(r, vofs, sofs, 0);
+    } else if constexpr (K == 2) {
+        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, vofs, sofs, 0);
+        v.r[0] = t[0];
+        v.r[1] = t[1];
+    } else {
+        static_assert(K % 4 == 0, "K = 1, 2 or a multiple of 4");
+#pragma unroll
+        for (int j = 0; j < K / 4; j++) {
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, vofs + 16 * j, sofs, 0);
+            v.r[4 * j] = t[0]; v.r[4 * j + 1] = t[1]; v.r[4 * j + 2] = t[2]; v.r[4 * j + 3] = t[3];
+        }
+    }
+    return v;
+}
+
+// non-temporal (aux = nt) stores of K packed pairs
+template <int K>
+__device__ __forceinline__ void store_buf_nt(Rsrc r, uint32_t vofs, uint32_t sofs, const Regs<K>& v) {
+    if constexpr (K == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(v.r[0], r, vofs, sofs, 2);
+    } else if constexpr (K == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) uint32_t){v.r[0], v.r[1]}, r,
+                                              vofs, sofs, 2);
+    } else {
+#pragma unroll
+        for (int j = 0; j < K / 4; j++)
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (__attribute__((ext_vector_type(4))) uint32_t){v.r[4 * j], v.r[4 * j + 1], v.r[4 * j + 2],
+                                                               v.r[4 * j + 3]},
+                r, vofs + 16 * j, sofs, 2);
+    }
+}
+
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// Dispatch-order block index h (of n) -> logical index such that consecutive logical blocks share
+// an XCD (and its L2): blocks are dealt round-robin over the 8 XCDs, so h and h + 8 share one
+// (MI355X_MICROARCH.md, workgroup dispatch); the XCD of h % 8 gets a contiguous logical range.
+__device__ __forceinline__ int xcd_block(int h, int n) {
+    const int q = n >> 3, r = n & 7, x = h & 7, k = h >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
 
 // Compile-time unrolling of a step functor f(k, integral_constant<J>) over J = 0..N-1 (all steps)
 // or over the J with k0 + J <= klast (tail); J is the static ring slot of step k0 + J.

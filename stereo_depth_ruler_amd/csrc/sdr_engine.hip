@@ -105,6 +105,9 @@ int check_frame(const Eff& e) {
     // stays below 2^31 (num_records): the longest chain span, slack rows included, must fit
     if ((size_t)(g.H + 2 * sdr::kSouthPad) * (size_t)(g.W1 + 1) * g.D * 2 > (size_t)INT32_MAX)
         return fail(SDR_ERR_SIZE, "frame too large: a path chain spans more than 2 GiB of cost volume");
+    // k_cost addresses a frame's right-image planes (3 x 8 B per pixel) the same way
+    if ((size_t)g.H * g.W * 24 > (size_t)INT32_MAX)
+        return fail(SDR_ERR_SIZE, "frame too large: the right image's cost planes span more than 2 GiB");
     if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
     return SDR_OK;
 }
@@ -157,7 +160,7 @@ struct sdr_sgbm {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    Buf planesL, planesR, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz, keys2;
+    Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz, keys2;
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -225,7 +228,7 @@ static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
         aux = (size_t)st->size() * amax * std::max(g.W1, 0) * g.D * 2;
     }
     const size_t px = (size_t)g.W * g.H;
-    return (size_t)F * (6 * px * 8 + cells * 2 * npaths_of(e.mode) + aux + px * 2 * 3 + px * 4 +
+    return (size_t)F * (3 * px * 4 + 3 * px * 8 + cells * 2 * npaths_of(e.mode) + aux + px * 2 * 3 + px * 4 +
                         px * 4 * 2);
 }
 
@@ -268,8 +271,9 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     for (auto& s : stripes) amax = std::max(amax, s.aux_rows);
     const size_t aux_fstride = (size_t)stripes.size() * amax * g.W1 * g.D;
 
-    if ((rc = ensure(h->planesL, F * 3 * px * 8))) return rc;
+    if ((rc = ensure(h->planesL, F * 3 * px * 4))) return rc;
     if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
+    if ((rc = ensure(h->sink, sdr::cost_sink_bytes(g)))) return rc;
     // the path kernels' loads overrun a chain's ends by up to kSouthPad rows: slack both sides
     const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
     const size_t lslack = slack * (P - 1);
@@ -295,7 +299,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     int16_t* dlr = (int16_t*)h->dlr.p;
 
     sdr::Planes pl;
-    pl.L = (uint64_t*)h->planesL.p;
+    pl.L = (uint32_t*)h->planesL.p;
     pl.R = (uint64_t*)h->planesR.p;
     pl.fstrideL = pl.fstrideR = 3 * px;
     { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st); }
@@ -311,6 +315,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     ca.ylim = std::max(H - 1 - g.SH2, 0);
     ca.hh_bottom = e.mode == SDR_MODE_HH;
     ca.TY = 0;  // sized by launch_cost for one full pass of resident blocks
+    ca.sink = (int16_t*)h->sink.p;
     { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
     for (size_t s = 0; s < stripes.size(); s++) {
         const Stripe& sp = stripes[s];
@@ -473,7 +478,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (Buf* b : {&h->planesL, &h->planesR, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
+    for (Buf* b : {&h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})

@@ -39,7 +39,7 @@ struct Geometry {
 
 // ---- prefilter / cost volume (sdr_cost.hip) ----
 struct Planes {
-    uint64_t* L;        // [F][3][H][W] int16 splats: {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
+    uint32_t* L;        // [F][H][W][3] 16-bit halves: {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
     uint64_t* R;        // [F][3][H][W] int16 pairs (q(x) | q(x-1) << 16): {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
     size_t fstrideL, fstrideR;  // elements per frame
 };
@@ -54,7 +54,9 @@ struct CostArgs {
     int ylim;                // rows > ylim repeat row ylim (running sum stops updating)
     int hh_bottom;           // MODE_HH: rows y>0 with y+SH2>=H keep the initial P2
     int TY;                  // tile height (output rows)
+    int16_t* sink;           // cost_sink_bytes() of scratch: the stores of warm-up rows land here
 };
+size_t cost_sink_bytes(const Geometry& g);
 
 
 // ---- path aggregation (sdr_paths.hip) ----

@@ -268,6 +268,7 @@ def main():
                         for _ in range(world)]
                        for _ in range(2 * ns)]
     pending = [None] * (2 * ns)
+    sent = {}  # slot -> the tensor this rank handed to that slot's last gather
 
     def step(i):
         j = (i * batch) % (nf - batch + 1) if nf > batch else 0
@@ -286,8 +287,9 @@ def main():
                 src = as_bytes(res) if res.dtype != torch.uint8 else res
                 if gloo:
                     src = src.cpu()  # gloo gathers host tensors (synchronises this stream)
-                pending[slot] = dist.gather(src.reshape(-1).clone() if kind != "sgbm" else src,
-                                            gather_bufs[slot] if rank == 0 else None, dst=0,
+                src = src.reshape(-1).clone() if kind != "sgbm" else src
+                sent[slot] = src
+                pending[slot] = dist.gather(src, gather_bufs[slot] if rank == 0 else None, dst=0,
                                             async_op=True)
 
     for i in range(a.warmup):
@@ -318,6 +320,20 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    gather_check = None
+    if world > 1:
+        # end-to-end check of the data path (after the timed region): rank 0's copy of every rank's
+        # bytes from the last timed step equals what that rank sent (position-weighted checksums)
+        def cks(b):
+            b = b.reshape(-1).to(torch.int64)
+            return int((b * (torch.arange(b.numel(), device=b.device) % 251 + 1)).sum())
+
+        last_slot = (a.warmup + a.steps - 1) % (2 * ns)
+        sums = [None] * world
+        dist.all_gather_object(sums, cks(sent[last_slot]))
+        if rank == 0:
+            gather_check = {"step": a.warmup + a.steps - 1, "ranks": world,
+                            "ok": all(cks(gather_bufs[last_slot][r]) == sums[r] for r in range(world))}
 
     Wm, Hm = (W // 2, H // 2) if kind == "live" else (W, H)  # the left matcher's frame
     w1 = Wm - max(args[0] + D, 0) + min(args[0], 0)
@@ -429,6 +445,7 @@ def main():
             "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),
+        "gather_check": gather_check,
         "roofline": roofline,
         "kernels": kernels,
         "cpu_baseline": None,

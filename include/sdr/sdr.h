@@ -91,9 +91,22 @@ int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);
 
 /* Host-pointer compute (H2D, compute, D2H, synchronous): left/right 8-bit, `stride` bytes per
- * row; disp int16 (1/16 px), `disp_stride` ELEMENTS per row. */
+ * row; disp int16 (1/16 px), `disp_stride` ELEMENTS per row.  Replaces StereoSGBM::compute on
+ * host cv::Mat (stereo_disparity.cpp:27-34, pcd_write.cpp:111).  The copies go through the
+ * handle's persistent page-locked staging in ~1 MB row chunks that overlap the CPU copy with the
+ * DMA; no allocation per call once the handle has seen the frame size. */
 int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int width, int height,
                      int channels, size_t stride, int16_t* disp, size_t disp_stride);
+
+/* Host-pointer form of the fused hot path of pcd_write.cpp:111-116 (synchronous): compute ->
+ * convertTo(CV_32F, 1/16) -> reprojectImageTo3D(Q, handle_missing) with the disparity kept on
+ * the device; xyz float32x3 rows of `xyz_stride` ELEMENTS (>= 3*width).  disp (optional, may be
+ * NULL) receives the int16 disparity as sdr_sgbm_compute would, its copy-out overlapping the
+ * reprojection. */
+int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int width,
+                               int height, size_t stride, int16_t* disp, size_t disp_stride,
+                               const double Q[16], int handle_missing, float* xyz,
+                               size_t xyz_stride);
 
 /* Device-pointer batch compute, asynchronous on the handle's stream: nframes frames spaced
  * frame_stride bytes (inputs) / disp_frame_stride elements (output) apart. */
@@ -109,7 +122,8 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* d_left, const 
                                       int nframes, int16_t* d_disp, const double Q[16],
                                       int handle_missing, float* d_xyz);
 
-/* reprojectImageTo3D on a CV_32F disparity (host pointers, synchronous). */
+/* reprojectImageTo3D on a CV_32F disparity (host pointers, synchronous; per-thread persistent
+ * device buffers and page-locked staging, no allocation per call). */
 int sdr_reproject(const float* disp, int width, int height, size_t disp_stride, const double Q[16],
                   int handle_missing, float* xyz, size_t xyz_stride);
 /* Device versions (asynchronous on `stream`, a hipStream_t; NULL = default stream). */
@@ -342,6 +356,12 @@ int sdr_selftest_wave_ops(int* failures4);
  * 5 = the fused WTA pass's per-pixel (minS << 16 | bestDisp) [F][H][W] u32, indexed by matched
  * column (0xffffffff: rejected); stage 1 holds values only in the matched columns. */
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
+
+/* Page-locked host memory (the role of cv::cuda::HostMem): host buffers from sdr_host_alloc that
+ * are passed to the host-pointer entry points are copied to and from by DMA directly, without
+ * the staging copy pageable memory needs. */
+int sdr_host_alloc(size_t bytes, void** out);
+int sdr_host_free(void* p);
 
 const char* sdr_last_error(void);
 int sdr_abi_version(void);

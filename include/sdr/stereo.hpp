@@ -71,8 +71,21 @@ public:
         if (data && r == rows && c == cols && t == type) return;
         rows = r; cols = c; type = t;
         step = (size_t)c * elem_size(t);
-        store_ = std::make_shared<std::vector<uint8_t>>((size_t)r * step);
-        data = store_->data();
+        auto v = std::make_shared<std::vector<uint8_t>>((size_t)r * step);
+        data = v->data();
+        store_ = v;
+    }
+    // page-locked storage (cv::cuda::HostMem(PAGE_LOCKED).createMatHeader()): the host-pointer
+    // calls DMA straight to and from it instead of staging a copy
+    static Mat page_locked(int r, int c, int t) {
+        Mat m;
+        m.rows = r; m.cols = c; m.type = t;
+        m.step = (size_t)c * elem_size(t);
+        void* p = nullptr;
+        check(sdr_host_alloc(std::max<size_t>((size_t)r * m.step, 1), &p));
+        m.store_ = std::shared_ptr<void>(p, [](void* q) { sdr_host_free(q); });
+        m.data = (uint8_t*)p;
+        return m;
     }
     bool empty() const { return !data || rows == 0 || cols == 0; }
     template <typename T> T* ptr(int y) { return (T*)(data + (size_t)y * step); }
@@ -85,10 +98,18 @@ public:
     }
 
 private:
-    std::shared_ptr<std::vector<uint8_t>> store_;
+    std::shared_ptr<void> store_;
 };
 
 template <class T> using Ptr = std::shared_ptr<T>;
+
+// Q (4x4, CV_64F or CV_32F) as 16 doubles
+inline void q_of(const Mat& Q, double q[16]) {
+    if (Q.rows != 4 || Q.cols != 4) throw Exception(SDR_ERR_ARG, "Q must be 4x4");
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+            q[i * 4 + j] = Q.type == CV_64FC1 ? Q.ptr<double>(i)[j] : (double)Q.ptr<float>(i)[j];
+}
 
 class StereoSGBM {
 public:
@@ -123,6 +144,23 @@ public:
         disparity.create(left.rows, left.cols, CV_16SC1);
         check(sdr_sgbm_compute(h_, left.data, right.data, left.cols, left.rows, 1, left.step,
                                (int16_t*)disparity.data, disparity.step / 2));
+    }
+
+    // compute -> convertTo(CV_32F, 1/16) -> reprojectImageTo3D(Q, handleMissingValues) in one call
+    // (pcd_write.cpp:111-116), the float disparity kept on the device; xyz CV_32FC3
+    void computeReproject(const Mat& left, const Mat& right, const Mat& Q, bool handleMissingValues,
+                          Mat& disparity, Mat& xyz) {
+        if (left.rows != right.rows || left.cols != right.cols || left.type != right.type)
+            throw Exception(SDR_ERR_ARG, "left and right images must have the same size and type");
+        if (left.type != CV_8UC1 || left.step != right.step)
+            throw Exception(SDR_ERR_TYPE, "8-bit single-channel images with equal steps are required");
+        double q[16];
+        q_of(Q, q);
+        disparity.create(left.rows, left.cols, CV_16SC1);
+        xyz.create(left.rows, left.cols, CV_32FC3);
+        check(sdr_sgbm_compute_reproject(h_, left.data, right.data, left.cols, left.rows, left.step,
+                                         (int16_t*)disparity.data, disparity.step / 2, q,
+                                         handleMissingValues ? 1 : 0, (float*)xyz.data, xyz.step / 4));
     }
 
     int getMinDisparity() const { return p_.minDisparity; }
@@ -174,11 +212,8 @@ inline void convertTo32F(const Mat& disp16, Mat& f, double scale) {
 
 inline void reprojectImageTo3D(const Mat& disparity, Mat& xyz, const Mat& Q,
                                bool handleMissingValues = false) {
-    if (Q.rows != 4 || Q.cols != 4) throw Exception(SDR_ERR_ARG, "Q must be 4x4");
     double q[16];
-    for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++)
-            q[i * 4 + j] = Q.type == CV_64FC1 ? Q.ptr<double>(i)[j] : (double)Q.ptr<float>(i)[j];
+    q_of(Q, q);
     Mat f = disparity;
     if (disparity.type == CV_16SC1) {  // OpenCV reads CV_16S values as-is (no 1/16 scaling)
         f = Mat(disparity.rows, disparity.cols, CV_32FC1);

@@ -5,7 +5,7 @@ HIP/CDNA4 kernels behind a C ABI (include/sdr/sdr.h), with an OpenCV-shaped Pyth
 from ._lib import SDRError, SgbmParams, WlsParams, LIB_PATH  # noqa: F401
 from .sgbm import (  # noqa: F401
     MODE_HH, MODE_HH4, MODE_SGBM, MODE_SGBM_3WAY, StereoSGBM, createRightMatcher,
-    cvt_bgr2gray, disparity_to_float, filterSpeckles, reprojectImageTo3D, resize_area_half,
+    cvt_bgr2gray, disparity_to_float, filterSpeckles, host_empty, reprojectImageTo3D, resize_area_half,
 )
 from . import cloud  # noqa: F401
 from . import display  # noqa: F401
@@ -20,5 +20,5 @@ __all__ = [
     "disparity_to_float", "filterSpeckles", "cvt_bgr2gray", "resize_area_half",
     "MODE_SGBM", "MODE_HH", "MODE_SGBM_3WAY", "MODE_HH4", "WlsParams", "DisparityWLSFilter",
     "createDisparityWLSFilter", "fastGlobalSmootherFilter", "StereoDisparity", "Display",
-    "colormap_lut", "COLORMAP_JET", "COLORMAP_TURBO",
+    "colormap_lut", "COLORMAP_JET", "COLORMAP_TURBO", "host_empty",
 ]

@@ -16,6 +16,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -155,12 +157,152 @@ int sdr::ensure(Buf& b, size_t bytes) {
     return SDR_OK;
 }
 
+namespace {
+// Page-locked staging for the host-pointer entry points, kept by its owner across calls (no
+// allocation per call).  Copies go through it in row chunks of about kXferChunk bytes: on the way
+// in, the CPU copy of chunk i+1 overlaps the DMA of chunk i; on the way out, every chunk's DMA is
+// queued behind the compute with an event, and the CPU copies chunk i out while chunk i+1 is
+// still on the link.
+constexpr size_t kXferChunk = (size_t)1 << 20;  // (256 KB and 4-16 MB chunks measured slower)
+// page-locked blocks handed out by sdr_host_alloc: base -> size
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pinned;
+// [p, p + bytes) lies inside one sdr_host_alloc block
+static bool is_pinned(const void* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pinned.upper_bound((uintptr_t)p);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    return (uintptr_t)p + bytes <= it->first + it->second;
+}
+// 2-D copy, as one linear copy when both sides are dense
+static hipError_t copy2d(void* dst, size_t dp, const void* src, size_t sp, size_t rb, int rows,
+                         hipMemcpyKind kind, hipStream_t st) {
+    if (dp == rb && sp == rb) return hipMemcpyAsync(dst, src, rb * rows, kind, st);
+    return hipMemcpy2DAsync(dst, dp, src, sp, rb, rows, kind, st);
+}
+struct HostXfer {
+    char* pin = nullptr;
+    size_t cap = 0, used = 0;
+    std::vector<hipEvent_t> ev;
+    size_t nev = 0;
+    struct Out {
+        char* dst;
+        size_t dpitch, rowbytes;
+        const char* src;  // in pin
+        int rows;
+        size_t ev;        // event index
+    };
+    std::vector<Out> outs;
+
+    // start a call needing `bytes` of staging
+    int begin(size_t bytes) {
+        used = 0;
+        nev = 0;
+        outs.clear();
+        if (bytes <= cap) return SDR_OK;
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        cap = 0;
+        if (hipHostMalloc((void**)&pin, bytes, hipHostMallocDefault) != hipSuccess) {
+            pin = nullptr;
+            return fail(SDR_ERR_NOMEM, "hipHostMalloc failed");
+        }
+        cap = bytes;
+        return SDR_OK;
+    }
+    char* take(size_t bytes) {
+        char* p = pin + used;
+        used += (bytes + 255) & ~(size_t)255;
+        return p;
+    }
+    int event(size_t* idx) {
+        if (nev == ev.size()) {
+            hipEvent_t e = nullptr;
+            SDR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ev.push_back(e);
+        }
+        *idx = nev++;
+        return SDR_OK;
+    }
+    // host rows (src, spitch) -> device rows (dst, dpitch), enqueued on st
+    int upload(void* dst, size_t dpitch, const void* src, size_t spitch, size_t rowbytes, int rows,
+               hipStream_t st) {
+        if (is_pinned(src, spitch * (rows - 1) + rowbytes)) {
+            SDR_HIP(copy2d(dst, dpitch, src, spitch, rowbytes, rows, hipMemcpyHostToDevice, st));
+            return SDR_OK;
+        }
+        char* stage = take(rowbytes * rows);
+        const int step = (int)std::max<size_t>(1, kXferChunk / rowbytes);
+        for (int r0 = 0; r0 < rows; r0 += step) {
+            const int n = std::min(step, rows - r0);
+            char* sp = stage + (size_t)r0 * rowbytes;
+            const char* hp = (const char*)src + (size_t)r0 * spitch;
+            if (spitch == rowbytes) std::memcpy(sp, hp, rowbytes * n);
+            else
+                for (int r = 0; r < n; r++) std::memcpy(sp + r * rowbytes, hp + r * spitch, rowbytes);
+            SDR_HIP(copy2d((char*)dst + (size_t)r0 * dpitch, dpitch, sp, rowbytes, rowbytes, n,
+                           hipMemcpyHostToDevice, st));
+        }
+        return SDR_OK;
+    }
+    // device rows (src, spitch) -> host rows (dst, dpitch): DMA chunks queued on st now, the
+    // host copies done by drain()
+    int download(void* dst, size_t dpitch, const void* src, size_t spitch, size_t rowbytes, int rows,
+                 hipStream_t st) {
+        if (is_pinned(dst, dpitch * (rows - 1) + rowbytes)) {
+            SDR_HIP(copy2d(dst, dpitch, src, spitch, rowbytes, rows, hipMemcpyDeviceToHost, st));
+            size_t e = 0;
+            int rc = event(&e);
+            if (rc) return rc;
+            SDR_HIP(hipEventRecord(ev[e], st));
+            outs.push_back({nullptr, 0, 0, nullptr, 0, e});  // nothing to copy: wait only
+            return SDR_OK;
+        }
+        char* stage = take(rowbytes * rows);
+        const int step = (int)std::max<size_t>(1, kXferChunk / rowbytes);
+        for (int r0 = 0; r0 < rows; r0 += step) {
+            const int n = std::min(step, rows - r0);
+            char* sp = stage + (size_t)r0 * rowbytes;
+            SDR_HIP(copy2d(sp, rowbytes, (const char*)src + (size_t)r0 * spitch, spitch, rowbytes, n,
+                           hipMemcpyDeviceToHost, st));
+            size_t e = 0;
+            int rc = event(&e);
+            if (rc) return rc;
+            SDR_HIP(hipEventRecord(ev[e], st));
+            outs.push_back({(char*)dst + (size_t)r0 * dpitch, dpitch, rowbytes, sp, n, e});
+        }
+        return SDR_OK;
+    }
+    int drain() {
+        for (const Out& o : outs) {
+            SDR_HIP(hipEventSynchronize(ev[o.ev]));
+            if (!o.dst) continue;
+            if (o.dpitch == o.rowbytes) std::memcpy(o.dst, o.src, o.rowbytes * o.rows);
+            else
+                for (int r = 0; r < o.rows; r++) std::memcpy(o.dst + r * o.dpitch, o.src + r * o.rowbytes, o.rowbytes);
+        }
+        outs.clear();
+        return SDR_OK;
+    }
+    void release() {
+        for (auto e : ev) (void)hipEventDestroy(e);
+        ev.clear();
+        if (pin) (void)hipHostFree(pin);
+        pin = nullptr;
+        cap = 0;
+    }
+};
+size_t stage_bytes(size_t n) { return (n + 255) & ~(size_t)255; }
+}  // namespace
+
 struct sdr_sgbm {
     sdr_sgbm_params p{};
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hdisp, hxyz, keys2;
+    Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hxyz, keys2;
+    HostXfer hx;  // pinned staging of the host-pointer entry points
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -479,10 +621,11 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (Buf* b : {&h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
-                   &h->labels, &h->sizes, &h->mins, &h->hin, &h->hdisp, &h->hxyz, &h->cls_bgr,
+                   &h->labels, &h->sizes, &h->mins, &h->hin, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})
         if (b->p) (void)hipFree(b->p);
+    h->hx.release();
     for (auto ev : h->ev)
         if (ev) (void)hipEventDestroy(ev);
     for (auto ev : h->kev) (void)hipEventDestroy(ev);
@@ -612,16 +755,51 @@ int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int
     SDR_HIP(hipSetDevice(h->device));
     const size_t px = (size_t)W * H;
     if ((rc = ensure(h->hin, 2 * px))) return rc;
+    if ((rc = h->hx.begin(2 * stage_bytes(px) + stage_bytes(px * 2)))) return rc;
     uint8_t* dL = (uint8_t*)h->hin.p;
     uint8_t* dR = dL + px;
-    SDR_HIP(hipMemcpy2DAsync(dL, W, left, stride, W, H, hipMemcpyHostToDevice, h->stream));
-    SDR_HIP(hipMemcpy2DAsync(dR, W, right, stride, W, H, hipMemcpyHostToDevice, h->stream));
+    if ((rc = h->hx.upload(dL, W, left, stride, W, H, h->stream))) return rc;
+    if ((rc = h->hx.upload(dR, W, right, stride, W, H, h->stream))) return rc;
     int16_t* fin = nullptr;
     if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, nullptr, &fin))) return rc;
-    SDR_HIP(hipMemcpy2DAsync(disp, disp_stride * 2, fin, W * 2, W * 2, H, hipMemcpyDeviceToHost,
-                             h->stream));
-    SDR_HIP(hipStreamSynchronize(h->stream));
-    return SDR_OK;
+    if ((rc = h->hx.download(disp, disp_stride * 2, fin, (size_t)W * 2, (size_t)W * 2, H, h->stream))) return rc;
+    return h->hx.drain();
+}
+
+int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int W, int H,
+                               size_t stride, int16_t* disp, size_t disp_stride, const double Q[16],
+                               int handle_missing, float* xyz, size_t xyz_stride) {
+    if (!h || !left || !right || !Q || !xyz) return fail(SDR_ERR_ARG, "null argument");
+    int rc = check_dims(W, H, stride, 1);
+    if (rc) return rc;
+    if (disp && disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
+    if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
+    SDR_HIP(hipSetDevice(h->device));
+    const size_t px = (size_t)W * H;
+    if ((rc = ensure(h->hin, 2 * px))) return rc;
+    if ((rc = ensure(h->hxyz, px * 12))) return rc;
+    if ((rc = ensure(h->mins, 4))) return rc;
+    if ((rc = h->hx.begin(2 * stage_bytes(px) + stage_bytes(px * 2) + stage_bytes(px * 12)))) return rc;
+    uint8_t* dL = (uint8_t*)h->hin.p;
+    uint8_t* dR = dL + px;
+    float* dX = (float*)h->hxyz.p;
+    if ((rc = h->hx.upload(dL, W, left, stride, W, H, h->stream))) return rc;
+    if ((rc = h->hx.upload(dR, W, right, stride, W, H, h->stream))) return rc;
+    int16_t* fin = nullptr;
+    int* mins = handle_missing ? (int*)h->mins.p : nullptr;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, mins, &fin))) return rc;
+    // the disparity's copy-out overlaps the reprojection
+    if (disp && (rc = h->hx.download(disp, disp_stride * 2, fin, (size_t)W * 2, (size_t)W * 2, H, h->stream)))
+        return rc;
+    {
+        KTimer kt(h, SDR_KERNEL_REPROJECT);
+        sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, mins, dX, (size_t)W * 3, px * 3, 1,
+                                  h->stream);
+    }
+    SDR_HIP(hipGetLastError());
+    retire(h);
+    if ((rc = h->hx.download(xyz, xyz_stride * 4, dX, (size_t)W * 12, (size_t)W * 12, H, h->stream))) return rc;
+    return h->hx.drain();
 }
 
 int sdr_reproject_device(const float* d_disp, int W, int H, size_t disp_stride, const double Q[16],
@@ -680,29 +858,77 @@ int sdr_disp16_reproject_device(const int16_t* d_disp, int W, int H, size_t disp
     return SDR_OK;
 }
 
+int sdr_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(SDR_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (!bytes) return fail(SDR_ERR_ARG, "zero size");
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
+        return fail(SDR_ERR_NOMEM, "hipHostMalloc failed");
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pinned[(uintptr_t)p] = bytes;
+    *out = p;
+    return SDR_OK;
+}
+
+int sdr_host_free(void* p) {
+    if (!p) return SDR_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pinned.find((uintptr_t)p);
+        if (it == g_pinned.end()) return fail(SDR_ERR_ARG, "not a block from sdr_host_alloc");
+        g_pinned.erase(it);
+    }
+    SDR_HIP(hipHostFree(p));
+    return SDR_OK;
+}
+
 int sdr_reproject(const float* disp, int W, int H, size_t disp_stride, const double Q[16],
                   int handle_missing, float* xyz, size_t xyz_stride) {
     if (!disp || !Q || !xyz) return fail(SDR_ERR_ARG, "null argument");
     int rc = check_dims(W, H, disp_stride, 1);
     if (rc) return rc;
     if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
-    const size_t px = (size_t)W * H;
-    float *dd = nullptr, *dx = nullptr;
-    SDR_HIP(hipMalloc(&dd, px * 4));
-    if (hipMalloc(&dx, px * 12) != hipSuccess) {
-        (void)hipFree(dd);
-        return fail(SDR_ERR_NOMEM, "hipMalloc failed");
+    // per-thread persistent device buffers, staging and stream (per current device)
+    struct State {
+        int device = -1;
+        hipStream_t st = nullptr;
+        Buf dd, dx, mins;
+        HostXfer hx;
+        ~State() {
+            if (device < 0) return;
+            (void)hipSetDevice(device);
+            if (st) (void)hipStreamSynchronize(st);
+            for (Buf* b : {&dd, &dx, &mins})
+                if (b->p) (void)hipFree(b->p);
+            hx.release();
+            if (st) (void)hipStreamDestroy(st);
+        }
+    };
+    static thread_local State S;
+    int dev = 0;
+    SDR_HIP(hipGetDevice(&dev));
+    if (S.device != dev) {
+        if (S.device >= 0) {
+            (void)hipSetDevice(S.device);
+            S.~State();
+            new (&S) State();
+            SDR_HIP(hipSetDevice(dev));
+        }
+        SDR_HIP(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+        S.device = dev;
     }
-    rc = SDR_OK;
-    if (hipMemcpy2D(dd, W * 4, disp, disp_stride * 4, W * 4, H, hipMemcpyHostToDevice) != hipSuccess)
-        rc = fail(SDR_ERR_DEVICE, "H2D failed");
-    if (!rc) rc = sdr_reproject_device(dd, W, H, W, Q, handle_missing, dx, (size_t)W * 3, 1, nullptr);
-    if (!rc && hipMemcpy2D(xyz, xyz_stride * 4, dx, (size_t)W * 12, (size_t)W * 12, H,
-                           hipMemcpyDeviceToHost) != hipSuccess)
-        rc = fail(SDR_ERR_DEVICE, "D2H failed");
-    (void)hipFree(dd);
-    (void)hipFree(dx);
-    return rc;
+    const size_t px = (size_t)W * H;
+    if ((rc = ensure(S.dd, px * 4)) || (rc = ensure(S.dx, px * 12)) || (rc = ensure(S.mins, 4))) return rc;
+    if ((rc = S.hx.begin(stage_bytes(px * 4) + stage_bytes(px * 12)))) return rc;
+    float* dd = (float*)S.dd.p;
+    float* dx = (float*)S.dx.p;
+    if ((rc = S.hx.upload(dd, (size_t)W * 4, disp, disp_stride * 4, (size_t)W * 4, H, S.st))) return rc;
+    sdr::launch_reproject_f32(dd, W, H, W, px, Q, handle_missing, handle_missing ? (int*)S.mins.p : nullptr, dx,
+                              (size_t)W * 3, px * 3, 1, S.st);
+    SDR_HIP(hipGetLastError());
+    if ((rc = S.hx.download(xyz, xyz_stride * 4, dx, (size_t)W * 12, (size_t)W * 12, H, S.st))) return rc;
+    return S.hx.drain();
 }
 
 int sdr_disp16_to_float_device(const int16_t* d_disp, float* d_out, size_t n, void* stream) {

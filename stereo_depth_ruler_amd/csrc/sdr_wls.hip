@@ -13,7 +13,7 @@
 //   k_wls_conf     left discontinuity (inline) + discontinuity-aware LR check -> confidence
 //                  x255 (full map for getConfidenceMap) and the two FGS inputs conf*d, conf,
 //                  compacted to the ROI
-//   k_fgs_sweep(2) one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
+//   k_fgs_sweep   one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
 //                  BOTH inputs at once (the elimination coefficients depend only on the guide
 //                  and lambda).  Lane = line over k-major data (coalesced), loads PF samples
 //                  ahead in registers, so a step costs the t-recurrence's division latency
@@ -136,147 +136,16 @@ __global__ __launch_bounds__(256) void k_wls_conf(const int16_t* __restrict__ dl
 // moves both right-hand sides between the two (LDS tiles).  Each lane walks its line with the
 // loads of the next PF samples in flight (register ring), so a step costs the dependent-division
 // latency of the t recurrence, not a memory round trip.
-#ifndef SDR_FGS_PF
-#define SDR_FGS_PF 8  // samples each lane loads ahead in the line solves
-#endif
-constexpr int kFgsPF = SDR_FGS_PF;
+constexpr int kFgsPF = 8;  // samples each lane loads ahead in the line solves
 
-#ifndef SDR_FGS_SHARED_RCP
-// the step's three divisions share one refined reciprocal (1) or are plain IEEE divisions (0):
-// bit-exact either way on MI355X, and C4 single-stream ran 800 fps with both, so the sweep's step
-// is not bound by the division chain; plain divisions stay the default
-#define SDR_FGS_SHARED_RCP 0
-#endif
-// num / den, correctly rounded, for the Thomas step's operands: |den| >= 1 (diagonally dominant
-// system) and moderate numerators, where v_div_scale leaves both operands unscaled and
-// v_div_fixup passes the quotient through.  The compiler's IEEE division is then exactly
-// rcp -> one Newton step -> q = n*r -> two residual corrections; the first three ops depend only
-// on den, so the t, p0 and p1 quotients of a step share them (and the serial t-chain loses the
-// scale and fixup ops).
-struct FgsRcp {
-    float d, r;
-};
-__device__ __forceinline__ FgsRcp fgs_rcp(float d) {
-    float r = __builtin_amdgcn_rcpf(d);
-    const float e = __builtin_fmaf(-d, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-    return {d, r};
-}
-__device__ __forceinline__ float fgs_div(float n, FgsRcp R) {
-    if constexpr (!SDR_FGS_SHARED_RCP) return n / R.d;
-    float q = n * R.r;
-    float rem = __builtin_fmaf(-R.d, q, n);
-    q = __builtin_fmaf(rem, R.r, q);
-    rem = __builtin_fmaf(-R.d, q, n);
-    return __builtin_fmaf(rem, R.r, q);
-}
-
-__global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1, const float* __restrict__ Cw,
-                                                  float* __restrict__ T, int nlines, int n,
-                                                  size_t fstride, float lam) {
-    constexpr int PF = kFgsPF;
-    const int l = blockIdx.x * 64 + threadIdx.x;
-    if (l >= nlines) return;
-    const size_t base = (size_t)blockIdx.y * fstride + l;
-    float* u0 = U0 + base;
-    float* u1 = U1 ? U1 + base : nullptr;
-    const float* cw = Cw + base;
-    float* t = T + base;
-    const size_t st = (size_t)nlines;
-    const int last = n - 1;
-    // ---- forward elimination ----
-    float r0[PF], r1[PF], rc[PF];
-#pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const size_t o = (size_t)min(j, last) * st;
-        r0[j] = u0[o];
-        r1[j] = u1 ? u1[o] : 0.0f;
-        rc[j] = cw[o];
-    }
-    float cprev = 0.0f, tprev = 0.0f, p0 = 0.0f, p1 = 0.0f;
-    for (int k0 = 0; k0 < n; k0 += PF) {
-        float n0[PF], n1[PF], nc[PF];
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const size_t o = (size_t)min(k0 + PF + j, last) * st;
-            n0[j] = u0[o];
-            n1[j] = u1 ? u1[o] : 0.0f;
-            nc[j] = cw[o];
-        }
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const int k = k0 + j;
-            if (k <= last) {
-                const size_t o = (size_t)k * st;
-                if (k == 0) {
-                    const float c0 = lam * rc[j];
-                    const FgsRcp den = fgs_rcp(1.0f - c0);
-                    tprev = fgs_div(c0, den);
-                    p0 = fgs_div(r0[j], den);
-                    if (u1) p1 = fgs_div(r1[j], den);
-                } else {
-                    const float aa = lam * cprev;
-                    const float c = lam * rc[j];
-                    const FgsRcp den = fgs_rcp((1.0f - c) - aa * (1.0f + tprev));
-                    tprev = fgs_div(c, den);
-                    p0 = fgs_div(r0[j] - aa * p0, den);
-                    if (u1) p1 = fgs_div(r1[j] - aa * p1, den);
-                }
-                cprev = rc[j];
-                t[o] = tprev;
-                u0[o] = p0;
-                if (u1) u1[o] = p1;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < PF; j++) { r0[j] = n0[j]; r1[j] = n1[j]; rc[j] = nc[j]; }
-    }
-    // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
-    float q0 = p0, q1 = p1;
-    float b0[PF], b1[PF], bt[PF];
-#pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const size_t o = (size_t)max(last - 1 - j, 0) * st;
-        b0[j] = u0[o];
-        b1[j] = u1 ? u1[o] : 0.0f;
-        bt[j] = t[o];
-    }
-    for (int k0 = last - 1; k0 >= 0; k0 -= PF) {
-        float n0[PF], n1[PF], nt[PF];
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const size_t o = (size_t)max(k0 - PF - j, 0) * st;
-            n0[j] = u0[o];
-            n1[j] = u1 ? u1[o] : 0.0f;
-            nt[j] = t[o];
-        }
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const int k = k0 - j;
-            if (k >= 0) {
-                const size_t o = (size_t)k * st;
-                q0 = b0[j] - bt[j] * q0;
-                u0[o] = q0;
-                if (u1) {
-                    q1 = b1[j] - bt[j] * q1;
-                    u1[o] = q1;
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < PF; j++) { b0[j] = n0[j]; b1[j] = n1[j]; bt[j] = nt[j]; }
-    }
-}
-
-#ifndef SDR_FGS_V2
-#define SDR_FGS_V2 1  // branch-light line solve (0: the first version above)
-#endif
-// The same line solve without per-sample branches: the second right-hand side is a template
-// parameter, the first sample uses the general step (with cprev = tprev = p = 0 it computes
+// The line solve has no per-sample branches: the second right-hand side is a template parameter,
+// the first sample uses the general step (with cprev = tprev = p = 0 it computes
 // den = (1 - c) - 0, t = c / den, p = (r - 0) / den: the k = 0 formulas, bit for bit), and only
-// the last, partial batch of PF samples checks the line's end.
+// the last, partial batch of PF samples checks the line's end.  The step's divisions are plain
+// IEEE divisions (a shared refined reciprocal was bit-exact too, and no faster: the sweep is not
+// bound by the division chain).
 template <bool U1>
-__global__ __launch_bounds__(64) void k_fgs_sweep2(float* U0, float* U1p, const float* __restrict__ Cw,
+__global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const float* __restrict__ Cw,
                                                    float* __restrict__ T, int nlines, int n,
                                                    size_t fstride, float lam) {
     constexpr int PF = kFgsPF;
@@ -467,12 +336,8 @@ struct FgsScratch {
 
 static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const float* Cw, float* T,
                       int nlines, int n, size_t fs, float lam) {
-    if constexpr (SDR_FGS_V2) {
-        if (U1) hipLaunchKernelGGL((k_fgs_sweep2<true>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
-        else hipLaunchKernelGGL((k_fgs_sweep2<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
-    } else {
-        hipLaunchKernelGGL(k_fgs_sweep, grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
-    }
+    if (U1) hipLaunchKernelGGL((k_fgs_sweep<true>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
+    else hipLaunchKernelGGL((k_fgs_sweep<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
 }
 
 static void launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,

@@ -173,8 +173,13 @@ class StereoSGBM:
         return out[0] if squeeze and disp is None else out
 
     def compute_reproject(self, left, right, Q, handleMissingValues=False, disp=None, xyz=None):
-        """Fused pcd_write.cpp:111-116 hot path on device: compute -> /16 -> reprojectImageTo3D.
-        Returns (disp int16 (F,H,W), xyz float32 (F,H,W,3))."""
+        """Fused pcd_write.cpp:111-116 hot path: compute -> /16 -> reprojectImageTo3D.
+
+        torch CUDA inputs: on device, returns (disp int16 (F,H,W), xyz float32 (F,H,W,3)).
+        numpy (H, W) inputs: the synchronous host-pointer call (sdr_sgbm_compute_reproject),
+        returns (disp int16 (H,W), xyz float32 (H,W,3)) as numpy; disp=False skips the disparity."""
+        if not (_is_cuda(left) or _is_cuda(right)):
+            return self._compute_reproject_host(left, right, Q, handleMissingValues, disp, xyz)
         left, right = self._prep_device(left, right)
         f, h, w = left.shape
         if disp is None:
@@ -186,6 +191,24 @@ class StereoSGBM:
             self._h, left.data_ptr(), right.data_ptr(), w, h, w, w * h, f, disp.data_ptr(), _Q(Q),
             int(bool(handleMissingValues)), xyz.data_ptr()))
         return disp, xyz
+
+    def _compute_reproject_host(self, left, right, Q, hm, disp, xyz):
+        left, right = np.asarray(left), np.asarray(right)
+        if left.shape != right.shape or left.dtype != np.uint8 or right.dtype != np.uint8 or left.ndim != 2:
+            raise SDRError(-5, "expected two 8-bit single-channel (H, W) images")
+        left, right = np.ascontiguousarray(left), np.ascontiguousarray(right)
+        h, w = left.shape
+        if disp is None:
+            disp = np.empty((h, w), np.int16)
+        if xyz is None:
+            xyz = np.empty((h, w, 3), np.float32)
+        for a, shape, dt in ((disp, (h, w), np.int16), (xyz, (h, w, 3), np.float32)):
+            if a is not False and (a.shape != shape or a.dtype != dt or not a.flags.c_contiguous):
+                raise SDRError(-1, f"output must be a C-contiguous {np.dtype(dt).name} {shape} array")
+        dptr = disp.ctypes.data if disp is not False else None
+        check(lib().sdr_sgbm_compute_reproject(self._h, left.ctypes.data, right.ctypes.data, w, h, w, dptr, w,
+                                               _Q(Q), int(bool(hm)), xyz.ctypes.data, w * 3))
+        return (disp if disp is not False else None), xyz
 
     def debug_stage(self, stage: int, shape, dtype):
         """Copy an internal buffer of the last compute (0 C, 1 raw WTA, 2 LR, 3 final, 4 path costs,
@@ -212,6 +235,20 @@ class StereoSGBM:
         a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
         check(lib().sdr_sgbm_last_timing(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return {"cost_ms": a.value, "paths_ms": b.value, "post_ms": c.value}
+
+
+def host_empty(shape, dtype) -> np.ndarray:
+    """A numpy array in page-locked host memory (sdr_host_alloc; the role of cv::cuda::HostMem).
+    Given to the host-pointer calls, it is copied by DMA directly, without a staging copy."""
+    import weakref
+    dt = np.dtype(dtype)
+    count = int(np.prod(shape))
+    n = max(count * dt.itemsize, 1)
+    p = ctypes.c_void_p()
+    check(lib().sdr_host_alloc(n, ctypes.byref(p)))
+    buf = (ctypes.c_char * n).from_address(p.value)
+    weakref.finalize(buf, lib().sdr_host_free, p.value)
+    return np.frombuffer(buf, dtype=dt, count=count).reshape(shape)
 
 
 def createRightMatcher(matcher_left: StereoSGBM) -> StereoSGBM:

@@ -39,6 +39,19 @@ int main(int argc, char** argv) {
         sdr::convertTo32F(disp, disp_float, 1.0 / 16.0);
         sdr::reprojectImageTo3D(disp_float, xyz, Q, true);
         dump(out + "/xyz.bin", xyz);
+        // the fused host call, into plain and into page-locked Mats: the same bytes
+        sdr::Mat disp2, xyz2;
+        sgbm->computeReproject(L, R, Q, true, disp2, xyz2);
+        sdr::Mat disp3 = sdr::Mat::page_locked(H, W, sdr::CV_16SC1), xyz3 = sdr::Mat::page_locked(H, W, sdr::CV_32FC3);
+        sdr::Mat Lp = sdr::Mat::page_locked(H, W, sdr::CV_8UC1), Rp = sdr::Mat::page_locked(H, W, sdr::CV_8UC1);
+        std::memcpy(Lp.data, l.data(), l.size());
+        std::memcpy(Rp.data, r.data(), r.size());
+        sgbm->computeReproject(Lp, Rp, Q, true, disp3, xyz3);
+        const size_t nd = (size_t)W * H * 2, nx = (size_t)W * H * 12;
+        std::printf("fused_equal=%d\n", std::memcmp(disp2.data, disp.data, nd) == 0 &&
+                                           std::memcmp(xyz2.data, xyz.data, nx) == 0 &&
+                                           std::memcmp(disp3.data, disp.data, nd) == 0 &&
+                                           std::memcmp(xyz3.data, xyz.data, nx) == 0);
         // class path: StereoDisparity(Q).computeDisparity(BGR, BGR) / computeDepth
         sdr::StereoDisparity sd(Q);
         sdr::Mat BL = sdr::Mat::view(H, W, sdr::CV_8UC3, bl.data()), BR = sdr::Mat::view(H, W, sdr::CV_8UC3, br.data());

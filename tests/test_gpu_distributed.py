@@ -1,0 +1,111 @@
+"""The N>1 path on the HIP engine, world size 2 on the box's one GPU: two fresh
+spawned processes (gloo, both ranks on cuda:0) each run the engine on their frame shard.
+
+  - gather_frames: rank 0's gathered disparities equal a single-process run of all frames on the
+    same engine, bit for bit (and the oracle on two of them);
+  - bench.py's own step/async-gather loop under torch.distributed.run (--dist-backend gloo): the
+    JSON line reports 2 ranks and its end-to-end gather check passes.
+
+Scaling is not measured here (both ranks share one GPU); the RCCL path is the same code with
+backend "nccl" and one GPU per rank.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = (0, 64, 5, 600, 2400, 1, 63, 12, 50, 2, 0)
+H, W, N = 96, 320, 7
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _frames():
+    from stereo_depth_ruler_amd import synthetic as S
+    return S.make_batch(N, H, W, 64, seed0=300)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import stereo_depth_ruler_amd as sdr
+    from stereo_depth_ruler_amd.distributed import gather_frames, shard_frames
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    Ls, Rs = _frames()
+    mine = shard_frames(N, world, rank)
+    m = sdr.StereoSGBM.create(*ARGS)
+    Ld = torch.from_numpy(Ls[mine]).cuda()
+    Rd = torch.from_numpy(Rs[mine]).cuda()
+    local = m.compute(Ld, Rd).cpu()  # gloo gathers host tensors
+    out = gather_frames(local, N, world, rank)
+    if rank == 0:
+        q.put(out.numpy())
+    dist.barrier()
+    m.close()
+    dist.destroy_process_group()
+
+
+def test_world2_gather_frames_hip_engine(oracle):
+    import torch.multiprocessing as mp
+
+    import stereo_depth_ruler_amd as sdr
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=150)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    Ls, Rs = _frames()
+    m = sdr.StereoSGBM.create(*ARGS)
+    single = m.compute(torch.from_numpy(Ls).cuda(), torch.from_numpy(Rs).cuda()).cpu().numpy()
+    assert got.shape == single.shape == (N, H, W)
+    assert np.array_equal(got, single)
+    p = oracle.make_params(*ARGS)
+    for i in (0, N - 1):
+        assert np.array_equal(got[i], oracle.sgbm_compute(Ls[i], Rs[i], p)), i
+
+
+def test_world2_bench_step_gather_loop():
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "2", "--dist-backend", "gloo", "--streams", "2",
+           "--frames", "4", "--no-cpu-baseline", "--no-kernel-timing"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["steps"] == 6
+    assert out["gather_check"] == {"step": 7, "ranks": 2, "ok": True}

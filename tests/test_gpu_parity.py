@@ -147,6 +147,12 @@ def test_full_size_c2_sgbm5_d128(oracle):
     assert np.array_equal(g.view(np.uint32), ref_xyz.view(np.uint32))
     fin = np.isfinite(ref_xyz)
     assert np.max(np.abs(g[fin] - ref_xyz[fin])) <= XYZ_TOL_MM
+    # the host-pointer forms (pinned staging, chunked copies) give the same bytes
+    hd, hx = m.compute_reproject(L, R, S.REFERENCE_Q, True)
+    assert np.array_equal(hd, got) and np.array_equal(hx.view(np.uint32), ref_xyz.view(np.uint32))
+    _, hx2 = m.compute_reproject(L, R, S.REFERENCE_Q, True, disp=False)
+    assert np.array_equal(hx2.view(np.uint32), ref_xyz.view(np.uint32))
+    assert np.array_equal(m.compute(L, R), got)
     # ground-truth sanity on the synthetic scene
     v = got > -16
     assert v.mean() > 0.8
@@ -312,6 +318,7 @@ def test_cpp_facade(oracle, tmp_path):
                          + [str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stderr
     assert "numDisparities=80" in res.stdout and "exception code=-2" in res.stdout
+    assert "fused_equal=1" in res.stdout
     disp = np.fromfile(tmp_path / "disp.bin", np.int16).reshape(H, W)
     ref = oracle.sgbm_compute(L, R, oracle.make_params(0, 80, 5, 600, 2400, 1, 63, 12, 200, 2, 2))
     assert np.array_equal(disp, ref)
@@ -340,3 +347,61 @@ def test_cpp_facade(oracle, tmp_path):
     assert np.array_equal(np.fromfile(tmp_path / "overlay.bin", np.uint8).reshape(h2, w2, 3), ov)
     cov = float(res.stdout.split("coverage=")[1].split()[0])
     assert cov == oracle.depth_coverage(depth, 80)
+
+
+def test_host_pointer_strides_and_sizes(oracle):
+    """sdr_sgbm_compute / sdr_sgbm_compute_reproject / sdr_reproject on padded host rows (stride >
+    width, output strides > width), and frame sizes that shrink and grow between calls (the
+    handle's pinned staging and device buffers only grow)."""
+    import ctypes
+
+    from stereo_depth_ruler_amd._lib import lib
+    args = (0, 48, 5, 600, 2400, 1, 63, 12, 50, 2, 0)
+    m = sdr.StereoSGBM.create(*args)
+    p = oracle.make_params(*args)
+    Q = (ctypes.c_double * 16)(*np.asarray(S.REFERENCE_Q, np.float64).ravel())
+    for (H, W, seed) in ((64, 200, 1), (40, 120, 2), (90, 333, 3)):
+        L, R, _ = S.make_pair(H, W, 48, seed=seed)
+        ref = oracle.sgbm_compute(L, R, p)
+        ref_xyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, True)
+        pad = 37
+        Lp = np.zeros((H, W + pad), np.uint8)
+        Rp = np.zeros((H, W + pad), np.uint8)
+        Lp[:, :W], Rp[:, :W] = L, R
+        dp = np.full((H, W + 5), 7, np.int16)
+        assert lib().sdr_sgbm_compute(m._h, Lp.ctypes.data, Rp.ctypes.data, W, H, 1, W + pad, dp.ctypes.data, W + 5) == 0
+        assert np.array_equal(dp[:, :W], ref) and (dp[:, W:] == 7).all()
+        xp = np.full((H, 3 * W + 4), 9, np.float32)
+        dp[:] = 7
+        assert lib().sdr_sgbm_compute_reproject(m._h, Lp.ctypes.data, Rp.ctypes.data, W, H, W + pad, dp.ctypes.data,
+                                                W + 5, Q, 1, xp.ctypes.data, 3 * W + 4) == 0
+        assert np.array_equal(dp[:, :W], ref) and (dp[:, W:] == 7).all()
+        assert np.array_equal(xp[:, :3 * W].reshape(H, W, 3).view(np.uint32), ref_xyz.view(np.uint32))
+        assert (xp[:, 3 * W:] == 9).all()
+        df = np.zeros((H, W + 3), np.float32)
+        df[:, :W] = oracle.disp_to_float(ref)
+        xp[:] = 9
+        assert lib().sdr_reproject(df.ctypes.data, W, H, W + 3, Q, 1, xp.ctypes.data, 3 * W + 4) == 0
+        assert np.array_equal(xp[:, :3 * W].reshape(H, W, 3).view(np.uint32), ref_xyz.view(np.uint32))
+    m.close()
+
+
+def test_host_pointer_page_locked_buffers(oracle):
+    """Page-locked caller buffers (sdr.host_empty) take the direct-DMA branch: same bytes."""
+    args = (0, 64, 5, 600, 2400, 1, 63, 12, 50, 2, 0)
+    H, W = 70, 250
+    L, R, _ = S.make_pair(H, W, 64, seed=5)
+    ref = oracle.sgbm_compute(L, R, oracle.make_params(*args))
+    ref_xyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, False)
+    pl, pr = sdr.host_empty((H, W), np.uint8), sdr.host_empty((H, W), np.uint8)
+    pl[:], pr[:] = L, R
+    pd, px = sdr.host_empty((H, W), np.int16), sdr.host_empty((H, W, 3), np.float32)
+    m = sdr.StereoSGBM.create(*args)
+    for _ in range(2):
+        pd[:] = 0
+        px[:] = 0
+        d, x = m.compute_reproject(pl, pr, S.REFERENCE_Q, False, disp=pd, xyz=px)
+        assert d is pd and x is px
+        assert np.array_equal(pd, ref) and np.array_equal(px.view(np.uint32), ref_xyz.view(np.uint32))
+        assert np.array_equal(m.compute(pl, pr, pd), ref)
+    m.close()

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+# SDR_ORACLE_LIB selects another build of the same sources (the ASan/UBSan one of `make asan`)
+_LIB_PATH = os.environ.get("SDR_ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
 MODE_SGBM, MODE_HH, MODE_SGBM_3WAY = 0, 1, 2

@@ -35,8 +35,13 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+HOST_ASAN = ["-g", "-fno-omit-frame-pointer"] + [x for f in ("-fsanitize=address", "-fsanitize=undefined",
+                                                            "-fno-sanitize-recover=undefined")
+                                                 for x in ("-Xarch_host", f)]
+
+
 def build_native(force: bool = False, verbose: bool = False, variant: str = "",
-                 defines: tuple = ()) -> str:
+                 defines: tuple = (), extra: tuple = ()) -> str:
     """Compiles each HIP source to an object in parallel (relocatable device code is not needed:
     every kernel is launched from the file that defines it), then links the shared library.
     variant/defines: an experiment build lib/libsdr-<variant>.so with extra -D switches."""
@@ -48,7 +53,7 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              "-Wall", "-Wno-unused-function", "-Wno-unused-result",
-             "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines]
+             "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines] + list(extra)
     hipcc = _hipcc()
     objs, procs = [], []
     for f in SOURCES:
@@ -61,7 +66,7 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
     failed = [cmd for cmd, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *extra, *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(link))
     subprocess.check_call(link)
@@ -73,7 +78,11 @@ if __name__ == "__main__":
     import sys
 
     # python build.py [variant NAME=V ...]  (-DNAME=V accepted too)
-    if len(sys.argv) > 1:
+    # python build.py --host-asan  -> lib/libsdr-asan.so, host code under ASan + UBSan (the device
+    #                                 code is unchanged: GPU sanitizers are not used on this pool)
+    if sys.argv[1:] == ["--host-asan"]:
+        print(build_native(force=True, variant="asan", extra=tuple(HOST_ASAN)))
+    elif len(sys.argv) > 1:
         defs = tuple(a[2:] if a.startswith("-D") else a for a in sys.argv[2:])
         print(build_native(force=True, variant=sys.argv[1], defines=defs))
     else:

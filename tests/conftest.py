@@ -10,6 +10,11 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) -- run with -m gpu")
+    # the sanitizer run (scripts/asan_cpu_suite.sh) points the tests at the host-ASan engine build
+    eng = os.environ.get("SDR_TEST_ENGINE_LIB")
+    if eng:
+        from stereo_depth_ruler_amd import _lib
+        _lib.use_library(eng)
 
 
 @pytest.fixture(scope="session")

@@ -214,8 +214,10 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 // 1 producer + 3 consumer waves (256 threads): the 1152 column chains of a 1280x720 d=128 frame
 // are resident in one pass.  2 and 4 consumer waves measured the same within noise.
 constexpr int kSouthConsumers = 3;
-constexpr int kSouthRB = 4 * kSouthConsumers;  // rows per block (4 per consumer wave)
-constexpr int kSouthLAB = 1;                   // producer lookahead in blocks
+constexpr int kSouthRPW = 4;                           // rows per consumer wave and block (4 per pass;
+                                                       // 8 rows x 2 consumers measured the same)
+constexpr int kSouthRB = kSouthRPW * kSouthConsumers;  // rows per block
+constexpr int kSouthLAB = 2;                   // producer lookahead in blocks (C0 -28 %, C2 -3 % vs 1)
 constexpr int kSouthSPad = 4;                  // dword padding of the consumers' staged S rows
 constexpr int kStageBlocks = 32;               // blocks per output staging window
 constexpr int kStageRows = kStageBlocks * kSouthRB;
@@ -229,15 +231,18 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     constexpr int RB = kSouthRB;
     constexpr int LAB = kSouthLAB;
     constexpr int LA = LAB * RB;  // producer lookahead in rows
-    constexpr int NS = 2 * LAB;   // ring blocks per producer loop body
-    constexpr int R = NS * RB;    // producer ring slots (rows)
+    // ring of LA slots, unrolled by LA steps: a slot is reloaded (row k + LA) as soon as row k
+    // is taken from it, so its register is static and never copied at the loop's back edge
+    constexpr int NS = LAB;       // ring blocks per producer loop body
+    constexpr int R = NS * RB;    // producer ring slots (rows) = LA
     static_assert(LA + RB <= kSouthPad, "load overrun must fit the buffers' row slack");
     constexpr int WDPL = DPL * 4;  // consumer: disparities per lane
     constexpr int WK = WDPL / 2;
     constexpr int DMAX = 64 * DPL;
     constexpr int LSTR = DMAX / 2 + 4;  // dwords per staged row (padded: rows of a wave's 4 pixels)
-    // consumer prefetch distance in blocks: the ring (2*PD blocks) of the other directions' L
-    constexpr int PD = NP * WK <= 8 ? 2 : 1;
+    // consumer prefetch distance in blocks (= ring slots) of the other directions' L
+    // (two blocks while the ring fits 64 VGPRs; 1 block -- a ring of 56 VGPRs -- for 8 paths at D > 128)
+    constexpr int PD = NP * WK * kSouthRPW <= 128 ? 2 : 1;
     static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
     __shared__ uint32_t sL[2][RB][LSTR];
     // each consumer row's S staged for the subpixel neighbours and the uniqueness minimum (one
@@ -309,18 +314,24 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         return;
     }
 
-    // ---------------- consumers: the other directions + WTA, 4 rows per wave ----------------
+    // ---------------- consumers: the other directions + WTA, RPW rows per wave ----------------
+    constexpr int NPASS = kSouthRPW / 4;  // passes of 4 rows (one per 16-lane group)
     const int gl = lane & 15, grp = lane >> 4;
-    const int r = (wv - 1) * 4 + grp;  // this lane group's row within a block
     const bool wactive = !PAD || gl * WDPL < D;
     const int wd0 = (PAD ? min(gl, D / WDPL - 1) : gl) * WDPL;
     // row blk*RB + r of the chain: wave-uniform block base + lane byte offset; the NP
     // directions of a pixel are one contiguous record (q*D*2 folds into the instruction offset)
     const ptrdiff_t bstepb = (ptrdiff_t)RB * W1 * pl.l_pix * 2;
-    const uint32_t lofs = (uint32_t)(((size_t)r * W1 * pl.l_pix + wd0) * 2);
+    int rr[NPASS];          // this lane group's row within a block, per pass
+    uint32_t lofs[NPASS];
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ps++) {
+        rr[ps] = (wv - 1) * kSouthRPW + ps * 4 + grp;
+        lofs[ps] = (uint32_t)(((size_t)rr[ps] * W1 * pl.l_pix + wd0) * 2);
+    }
     const char* lbase = (const char*)(a.L + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
-    auto oload = [&](int q, int blk) __attribute__((always_inline)) {
-        return load_buf<WK>(rsrc_at(lbase + (ptrdiff_t)blk * bstepb), lofs + (uint32_t)(q * D * 2));
+    auto oload = [&](int q, int blk, int ps) __attribute__((always_inline)) {
+        return load_buf<WK>(rsrc_at(lbase + (ptrdiff_t)blk * bstepb), lofs[ps] + (uint32_t)(q * D * 2));
     };
     // rows before kw belong to the previous 3WAY stripe: recurred through, never output
     const int kw = ch.kwrite;
@@ -346,23 +357,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         }
     };
 
-    // ring of 2*PD blocks loaded PD ahead (as the producer's: no copies at the back edge);
-    // unconditional: blocks past the chain's end read the buffers' row slack (kSouthPad)
-    constexpr int OR = 2 * PD;
-    Regs<WK> oring[OR][NP];
-#pragma unroll
-    for (int s = 0; s < PD; s++)
-#pragma unroll
-        for (int q = 0; q < NP; q++) oring[s][q] = oload(q, s);
-
-    auto consume_sync = [&](const int b, auto sc) __attribute__((always_inline)) {
-        constexpr int s = decltype(sc)::value;
-        Regs<WK> o[NP];
-#pragma unroll
-        for (int q = 0; q < NP; q++) o[q] = oring[s][q];
-#pragma unroll
-        for (int q = 0; q < NP; q++) oring[(s + PD) % OR][q] = oload(q, b + PD);
-        // S = sat(sum of the P path costs), the fused direction's L from LDS
+    // one 4-row pass of block b: S of row k = b*RB + r, the WTA, its outputs staged in LDS
+    // S = sat(sum of the P path costs) of row r of block b, the fused direction's L from LDS
+    auto ssum = [&](const int b, const int r, const Regs<WK> (&o)[NP]) __attribute__((always_inline)) {
         const uint32_t* ls = &sL[b & 1][r][wd0 / 2];
         Regs<WK> St;
 #pragma unroll
@@ -375,6 +372,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             }
             St.r[i] = acc;
         }
+        return St;
+    };
+    auto rows = [&](const int b, const int r, const Regs<WK>& St) __attribute__((always_inline)) {
         const int k = b * RB + r;
         const bool rowok = k >= kw && k <= last;
         // first minimum: packed (S + 32768) << 16 | d keys, min over the 16-lane row
@@ -432,6 +432,29 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             sRaw[(k / kStageRows) & 1][k % kStageRows] = (int16_t)out;
             sKey[(k / kStageRows) & 1][k % kStageRows] = okey;
         }
+    };
+
+    // ring of PD blocks: slot s holds block b (b = s mod PD) until its sum is taken, then the
+    // load of block b + PD goes into the same registers, so each block's loads have PD block
+    // periods to land (the loop is unrolled by PD: static slots, no copies at the back edge);
+    // unconditional: blocks past the chain's end read the buffers' row slack (kSouthPad)
+    Regs<WK> oring[PD][NPASS][NP];
+#pragma unroll
+    for (int s = 0; s < PD; s++)
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ps++)
+#pragma unroll
+            for (int q = 0; q < NP; q++) oring[s][ps][q] = oload(q, s, ps);
+
+    auto consume_sync = [&](const int b, auto sc) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ps++) {
+            const Regs<WK> St = ssum(b, rr[ps], oring[s][ps]);
+#pragma unroll
+            for (int q = 0; q < NP; q++) oring[s][ps][q] = oload(q, b + PD, ps);
+            rows(b, rr[ps], St);
+        }
         __syncthreads();
         // the window this block completes (or the chain's last, partial one) goes out now that
         // every consumer's rows of it are staged; its buffer is rewritten kStageBlocks blocks on
@@ -439,8 +462,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     };
     __syncthreads();  // block 0 staged
     int b = 0;
-    for (; b + OR <= nblk; b += OR) unroll_rows(consume_sync, b, std::make_integer_sequence<int, OR>{});
-    unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, OR - 1>{});
+    for (; b + PD <= nblk; b += PD) unroll_rows(consume_sync, b, std::make_integer_sequence<int, PD>{});
+    unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, PD>{});
 }
 
 // A.8's right-view WTA (disp2) and A.9, one workgroup per image row: the fused pass's

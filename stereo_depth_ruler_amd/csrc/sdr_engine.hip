@@ -544,14 +544,17 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
     { KTimer kt(h, SDR_KERNEL_LR_CHECK); sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st); }
     const bool speckle = e.speckle_ws > 0;
-    { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, speckle ? dfin : dst, W, H, F, st); }
     if (speckle) {
+        // the median filter runs inside the labelling's first pass (dfin = median of dlr)
         KTimer kt(h, SDR_KERNEL_SPECKLE);
         sdr::launch_speckle(dfin, dst, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
-                            (int*)h->labels.p, (int*)h->sizes.p, out_min, st);
-    } else if (out_min) {
-        KTimer kt(h, SDR_KERNEL_REPROJECT);
-        sdr::launch_min_s16(dst, px, px, F, out_min, st);
+                            (int*)h->labels.p, (int*)h->sizes.p, out_min, st, dlr, dfin);
+    } else {
+        { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, dst, W, H, F, st); }
+        if (out_min) {
+            KTimer kt(h, SDR_KERNEL_REPROJECT);
+            sdr::launch_min_s16(dst, px, px, F, out_min, st);
+        }
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
     retire(h);

@@ -113,9 +113,12 @@ bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
-// src may equal dst; out_min (nullable) receives min over each output frame
+// src may equal dst; out_min (nullable) receives min over each output frame.  median_of
+// (nullable): src is instead the 3x3 median of median_of, computed by the first pass and written
+// to median_out (= src) -- the median filter fused into the labelling
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
-                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st);
+                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st,
+                    const int16_t* median_of = nullptr, int16_t* median_out = nullptr);
 void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
                     hipStream_t st);
 void launch_reproject_s16(const int16_t* disp, int W, int H, size_t dstride, size_t dfstride,

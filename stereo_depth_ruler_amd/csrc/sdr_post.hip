@@ -11,26 +11,31 @@ namespace sdr {
 // ------------------------------------------------------------------------------------------
 // A.10 medianBlur 3x3, replicate border (Devillard's 19-exchange median-of-9 network)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src,
-                                                 int16_t* __restrict__ dst, int W, int H) {
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
-    const size_t fo = (size_t)blockIdx.z * W * H;
-    if (x >= W || y >= H) return;
+// 3x3 median at (x, y) of a frame, BORDER_REPLICATE (medianBlur ksize 3: 19-exchange network)
+__device__ __forceinline__ int median3_at(const int16_t* __restrict__ src, int W, int H, int x, int y) {
     int p[9];
     const int xs[3] = {max(x - 1, 0), x, min(x + 1, W - 1)};
     const int ys[3] = {max(y - 1, 0), y, min(y + 1, H - 1)};
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) p[i * 3 + j] = src[fo + (size_t)ys[i] * W + xs[j]];
+        for (int j = 0; j < 3; j++) p[i * 3 + j] = src[(size_t)ys[i] * W + xs[j]];
 #define SDR_S(a, b) { int t_ = min(p[a], p[b]); p[b] = max(p[a], p[b]); p[a] = t_; }
     SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 1) SDR_S(3, 4) SDR_S(6, 7)
     SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 3) SDR_S(5, 8) SDR_S(4, 7)
     SDR_S(3, 6) SDR_S(1, 4) SDR_S(2, 5) SDR_S(4, 7) SDR_S(4, 2) SDR_S(6, 4)
     SDR_S(4, 2)
 #undef SDR_S
-    dst[fo + (size_t)y * W + x] = (int16_t)p[4];
+    return p[4];
+}
+
+__global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src,
+                                                 int16_t* __restrict__ dst, int W, int H) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const size_t fo = (size_t)blockIdx.z * W * H;
+    if (x >= W || y >= H) return;
+    dst[fo + (size_t)y * W + x] = (int16_t)median3_at(src + fo, W, H, x, y);
 }
 
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st) {
@@ -119,10 +124,13 @@ __device__ __forceinline__ bool joined(int a, int b, int newVal, int maxDiff) {
     return a != newVal && b != newVal && abs(a - b) <= maxDiff;
 }
 
-// 256 threads = 4 waves; pixel i = t + 256k (k < 4): a wave covers two tile rows per k
-__global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ img, int* __restrict__ P,
-                                                   int* __restrict__ S, int W, int H, int newVal,
-                                                   int maxDiff, int* out_min) {
+// 256 threads = 4 waves; pixel i = t + 256k (k < 4): a wave covers two tile rows per k.
+// MED: img is the median filter's input; the tile's medians are computed here and written to
+// med (the image merge and apply read), which saves the median pass.
+template <bool MED>
+__global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ img, int16_t* __restrict__ med,
+                                                   int* __restrict__ P, int* __restrict__ S, int W, int H,
+                                                   int newVal, int maxDiff, int* out_min) {
     __shared__ int v[kCT * kCT];
     __shared__ int lab[kCT * kCT];
     __shared__ int cnt[kCT * kCT];
@@ -135,7 +143,15 @@ __global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ i
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int i = t + 256 * k, gy = ty0 + (i >> 5);
-        val[k] = (gx < W && gy < H) ? (int)img[fo + (size_t)gy * W + gx] : newVal;
+        if (MED) {
+            val[k] = newVal;
+            if (gx < W && gy < H) {
+                val[k] = median3_at(img + fo, W, H, gx, gy);
+                med[fo + (size_t)gy * W + gx] = (int16_t)val[k];
+            }
+        } else {
+            val[k] = (gx < W && gy < H) ? (int)img[fo + (size_t)gy * W + gx] : newVal;
+        }
         v[i] = val[k];
         cnt[i] = 0;
     }
@@ -268,10 +284,16 @@ __global__ __launch_bounds__(256) void k_ccl_apply(const int16_t* src, int16_t* 
 }
 
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
-                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st) {
+                    int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st,
+                    const int16_t* median_of, int16_t* median_out) {
     const int n = W * H;
-    hipLaunchKernelGGL(k_ccl_local, dim3((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, F), dim3(256), 0,
-                       st, src, labels, sizes, W, H, newVal, maxDiff, out_min);
+    const dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, F);
+    if (median_of)
+        hipLaunchKernelGGL((k_ccl_local<true>), tiles, dim3(256), 0, st, median_of, median_out, labels, sizes, W,
+                           H, newVal, maxDiff, out_min);
+    else
+        hipLaunchKernelGGL((k_ccl_local<false>), tiles, dim3(256), 0, st, src, (int16_t*)nullptr, labels, sizes,
+                           W, H, newVal, maxDiff, out_min);
     const int nb = ((W - 1) / kCT) * H + ((H - 1) / kCT) * W;
     if (nb > 0)
         hipLaunchKernelGGL(k_ccl_merge, dim3((unsigned)min((nb + 255) / 256, 1024), F), dim3(256), 0,

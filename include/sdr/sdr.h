@@ -47,9 +47,9 @@ enum {
     SDR_OK = 0,
     SDR_ERR_ARG = -1,         /* null pointer, non-positive size, bad stride */
     SDR_ERR_NUMDISP = -2,     /* numDisparities <= 0 or not a multiple of 16 (OpenCV assert) */
-    SDR_ERR_MODE = -3,        /* unsupported mode (MODE_HH4) */
+    SDR_ERR_MODE = -3,        /* unknown mode */
     SDR_ERR_SIZE = -4,        /* image too narrow for the disparity range / block size */
-    SDR_ERR_TYPE = -5,        /* channels != 1 (8-bit single channel, as the reference passes) */
+    SDR_ERR_TYPE = -5,        /* channels other than 1 or 3 (CV_8UC1 / CV_8UC3) */
     SDR_ERR_DEVICE = -6,      /* HIP runtime error */
     SDR_ERR_NOMEM = -7,
     SDR_ERR_LIMIT = -8        /* numDisparities > 256 (engine limit) */
@@ -90,8 +90,8 @@ int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
 int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);
 
-/* Host-pointer compute (H2D, compute, D2H, synchronous): left/right 8-bit, `stride` bytes per
- * row; disp int16 (1/16 px), `disp_stride` ELEMENTS per row.  Replaces StereoSGBM::compute on
+/* Host-pointer compute (H2D, compute, D2H, synchronous): left/right 8-bit with `channels` (1 or 3)
+ * interleaved channels, `stride` bytes per row; disp int16 (1/16 px), `disp_stride` ELEMENTS per row.  Replaces StereoSGBM::compute on
  * host cv::Mat (stereo_disparity.cpp:27-34, pcd_write.cpp:111).  The copies go through the
  * handle's persistent page-locked staging in ~1 MB row chunks that overlap the CPU copy with the
  * DMA; no allocation per call once the handle has seen the frame size. */
@@ -114,6 +114,14 @@ int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* d_left, const uint8_t* d
                             int width, int height, size_t stride, size_t frame_stride,
                             int nframes, int16_t* d_disp, size_t disp_stride,
                             size_t disp_frame_stride);
+
+/* sdr_sgbm_compute_device for 8-bit images with `channels` (1 or 3) interleaved channels (stride
+ * and frame_stride in bytes): StereoSGBM::compute on CV_8UC3 input, whose calcPixelCostBT sums each
+ * channel's Sobel and raw costs (stereosgbm.cpp, cn == 3 branch). */
+int sdr_sgbm_compute_device_cn(sdr_sgbm* h, const uint8_t* d_left, const uint8_t* d_right,
+                               int width, int height, int channels, size_t stride,
+                               size_t frame_stride, int nframes, int16_t* d_disp,
+                               size_t disp_stride, size_t disp_frame_stride);
 
 /* Fused hot path of point_cloud/src/pcd_write.cpp:111-116 on device: compute + convertTo(1/16)
  * + reprojectImageTo3D(Q, handle_missing) -> xyz float32x3 [nframes][height][width][3]. */

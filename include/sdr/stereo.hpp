@@ -135,15 +135,17 @@ public:
     StereoSGBM(const StereoSGBM&) = delete;
     StereoSGBM& operator=(const StereoSGBM&) = delete;
 
-    // StereoMatcher::compute: CV_8UC1 pair -> CV_16SC1 disparity (1/16 px); disp is (re)allocated
+    // StereoMatcher::compute: CV_8UC1 or CV_8UC3 pair -> CV_16SC1 disparity (1/16 px); disp is
+    // (re)allocated
     void compute(const Mat& left, const Mat& right, Mat& disparity) {
         if (left.rows != right.rows || left.cols != right.cols || left.type != right.type)
             throw Exception(SDR_ERR_ARG, "left and right images must have the same size and type");
-        if (left.type != CV_8UC1 || left.step != right.step)
-            throw Exception(SDR_ERR_TYPE, "8-bit single-channel images with equal steps are required");
+        if ((left.type != CV_8UC1 && left.type != CV_8UC3) || left.step != right.step)
+            throw Exception(SDR_ERR_TYPE, "8-bit 1- or 3-channel images with equal steps are required");
         disparity.create(left.rows, left.cols, CV_16SC1);
-        check(sdr_sgbm_compute(h_, left.data, right.data, left.cols, left.rows, 1, left.step,
-                               (int16_t*)disparity.data, disparity.step / 2));
+        check(sdr_sgbm_compute(h_, left.data, right.data, left.cols, left.rows,
+                               left.type == CV_8UC3 ? 3 : 1, left.step, (int16_t*)disparity.data,
+                               disparity.step / 2));
     }
 
     // compute -> convertTo(CV_32F, 1/16) -> reprojectImageTo3D(Q, handleMissingValues) in one call

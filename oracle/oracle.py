@@ -66,6 +66,10 @@ def lib():
         L.orc_sgbm_compute_stages.restype = ci
         L.orc_cost_volume.argtypes = [u8p, u8p, ci, ci, sz, ctypes.POINTER(OrcParams), i16p]
         L.orc_cost_volume.restype = ci
+        L.orc_sgbm_compute_cn.argtypes = [u8p, u8p, ci, ci, sz, ci, ctypes.POINTER(OrcParams), i16p, sz, ci]
+        L.orc_sgbm_compute_cn.restype = ci
+        L.orc_cost_volume_cn.argtypes = [u8p, u8p, ci, ci, sz, ci, ctypes.POINTER(OrcParams), i16p]
+        L.orc_cost_volume_cn.restype = ci
         L.orc_pixel_cost_row.argtypes = [u8p, u8p, ci, ci, sz, ci, ci, ci, ci, i16p]
         L.orc_pixel_cost_row.restype = ci
         L.orc_median3x3_s16.argtypes = [i16p, i16p, ci, ci]
@@ -120,11 +124,12 @@ def sgbm_compute(left: np.ndarray, right: np.ndarray, params: OrcParams,
                  stages: int = STAGE_MEDIAN | STAGE_SPECKLE) -> np.ndarray:
     left = np.ascontiguousarray(left, dtype=np.uint8)
     right = np.ascontiguousarray(right, dtype=np.uint8)
-    assert left.shape == right.shape and left.ndim == 2
-    h, w = left.shape
+    assert left.shape == right.shape and (left.ndim == 2 or (left.ndim == 3 and left.shape[2] == 3))
+    h, w = left.shape[:2]
+    cn = 1 if left.ndim == 2 else 3
     out = np.empty((h, w), np.int16)
-    rc = lib().orc_sgbm_compute_stages(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w,
-                                       ctypes.byref(params), _p(out, ctypes.c_int16), w, stages)
+    rc = lib().orc_sgbm_compute_cn(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w * cn, cn,
+                                   ctypes.byref(params), _p(out, ctypes.c_int16), w, stages)
     if rc != 0:
         raise ValueError(f"orc_sgbm_compute failed: {rc}")
     return out
@@ -133,12 +138,13 @@ def sgbm_compute(left: np.ndarray, right: np.ndarray, params: OrcParams,
 def cost_volume(left, right, params: OrcParams) -> np.ndarray:
     left = np.ascontiguousarray(left, dtype=np.uint8)
     right = np.ascontiguousarray(right, dtype=np.uint8)
-    h, w = left.shape
+    h, w = left.shape[:2]
+    cn = 1 if left.ndim == 2 else 3
     minD, D = params.minDisparity, params.numDisparities
     w1 = (w + min(minD, 0)) - max(minD + D, 0)
     out = np.empty((h, w1, D), np.int16)
-    rc = lib().orc_cost_volume(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w,
-                               ctypes.byref(params), _p(out, ctypes.c_int16))
+    rc = lib().orc_cost_volume_cn(_p(left, ctypes.c_uint8), _p(right, ctypes.c_uint8), w, h, w * cn, cn,
+                                  ctypes.byref(params), _p(out, ctypes.c_int16))
     if rc != 0:
         raise ValueError(f"orc_cost_volume failed: {rc}")
     return out

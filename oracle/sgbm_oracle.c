@@ -50,6 +50,7 @@ typedef struct eff_params {
     int uniq, disp12MaxDiff, ftzero;
     int uniq_simd;
     int invalid_scaled;
+    int cn;  /* interleaved channels of the input images (1 or 3) */
 } eff_params;
 
 static int make_eff(const orc_params* p, int width, eff_params* e)
@@ -78,6 +79,7 @@ static int make_eff(const orc_params* p, int width, eff_params* e)
     else if (p->uniq_rule == ORC_UNIQ_SIMD) e->uniq_simd = 1;
     else e->uniq_simd = (p->mode == ORC_MODE_SGBM_3WAY);
     e->invalid_scaled = (e->minD - 1) * DISP_SCALE;
+    e->cn = 1;
     return 0;
 }
 
@@ -91,24 +93,25 @@ static void make_clip_tab(int ftzero, uint8_t* tab /* TAB_OFS*2 + 256 */)
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* A.1 + A.2: calcPixelCostBT for one image row y.                                             */
+/* A.1 + A.2: calcPixelCostBT for one image row y of an 8-bit image with cn (1 or 3)           */
+/* interleaved channels.  Prefiltered channels 0..cn-1 are the per-channel x-Sobels (cost      */
+/* shift 0), cn..2cn-1 the raw channels (cost shift 2); the pixel cost sums all 2cn of them.   */
 /* cost: [width1][D], cost[(x-minX1)*D + (d-minD)] for x in [minX1,maxX1), d in [minD,maxD).   */
 /* ------------------------------------------------------------------------------------------ */
 static void calc_pixel_cost_bt(const uint8_t* img1, const uint8_t* img2, size_t step, int width,
                                int height, int y, int minD, int maxD, cost_t* cost,
-                               const uint8_t* tab /* centred at 0 */, uint8_t* work /* 6*width */)
+                               const uint8_t* tab /* centred at 0 */,
+                               uint8_t* work /* (4*cn + 2) * width */, int cn)
 {
     const int D = maxD - minD;
     const int minX1 = imax(maxD, 0), maxX1 = width + imin(minD, 0);
     const int width1 = maxX1 - minX1;
     const int minX2 = imax(minX1 - maxD, 0), maxX2 = imin(maxX1 - minD, width);
 
-    uint8_t* sob1 = work;               /* prefiltered (x-Sobel, clipped) left row   */
-    uint8_t* raw1 = work + width;       /* raw left row (borders replaced by tab[0]) */
-    uint8_t* sob2 = work + 2 * width;
-    uint8_t* raw2 = work + 3 * width;
-    uint8_t* v0b = work + 4 * width;    /* min(v, v half-left, v half-right) for the right row */
-    uint8_t* v1b = work + 5 * width;    /* max(...)                                           */
+    uint8_t* pre1 = work;                        /* [2cn][width] prefiltered left channels  */
+    uint8_t* pre2 = work + 2 * cn * width;       /* [2cn][width] prefiltered right channels */
+    uint8_t* v0b = work + 4 * cn * width;        /* min(v, v half-left, v half-right) for the right row */
+    uint8_t* v1b = work + (4 * cn + 1) * width;  /* max(...)                                           */
 
     const uint8_t* r1 = img1 + (size_t)y * step;
     const uint8_t* r2 = img2 + (size_t)y * step;
@@ -118,22 +121,29 @@ static void calc_pixel_cost_bt(const uint8_t* img1, const uint8_t* img2, size_t 
     const uint8_t* n2 = y > 0 ? r2 - step : r2;
     const uint8_t* s2 = y < height - 1 ? r2 + step : r2;
 
-    /* columns 0 and width-1 of every prefiltered channel (Sobel and raw) hold tab[0] */
-    sob1[0] = sob1[width - 1] = raw1[0] = raw1[width - 1] = tab[0];
-    sob2[0] = sob2[width - 1] = raw2[0] = raw2[width - 1] = tab[0];
-    for (int x = 1; x < width - 1; x++) {
-        sob1[x] = tab[(r1[x + 1] - r1[x - 1]) * 2 + n1[x + 1] - n1[x - 1] + s1[x + 1] - s1[x - 1]];
-        sob2[x] = tab[(r2[x + 1] - r2[x - 1]) * 2 + n2[x + 1] - n2[x - 1] + s2[x + 1] - s2[x - 1]];
-        raw1[x] = r1[x];
-        raw2[x] = r2[x];
+    for (int c = 0; c < cn; c++) {
+        uint8_t* sob1 = pre1 + c * width;
+        uint8_t* raw1 = pre1 + (cn + c) * width;
+        uint8_t* sob2 = pre2 + c * width;
+        uint8_t* raw2 = pre2 + (cn + c) * width;
+        /* columns 0 and width-1 of every prefiltered channel (Sobel and raw) hold tab[0] */
+        sob1[0] = sob1[width - 1] = raw1[0] = raw1[width - 1] = tab[0];
+        sob2[0] = sob2[width - 1] = raw2[0] = raw2[width - 1] = tab[0];
+        for (int x = 1; x < width - 1; x++) {
+            const int a = (x + 1) * cn + c, b = (x - 1) * cn + c;
+            sob1[x] = tab[(r1[a] - r1[b]) * 2 + n1[a] - n1[b] + s1[a] - s1[b]];
+            sob2[x] = tab[(r2[a] - r2[b]) * 2 + n2[a] - n2[b] + s2[a] - s2[b]];
+            raw1[x] = r1[x * cn + c];
+            raw2[x] = r2[x * cn + c];
+        }
     }
 
     for (int i = 0; i < width1 * D; i++) cost[i] = 0;
 
-    for (int c = 0; c < 2; c++) {
-        const uint8_t* p1 = c == 0 ? sob1 : raw1;
-        const uint8_t* p2 = c == 0 ? sob2 : raw2;
-        const int diff_scale = c == 0 ? 0 : 2;
+    for (int c = 0; c < 2 * cn; c++) {
+        const uint8_t* p1 = pre1 + c * width;
+        const uint8_t* p2 = pre2 + c * width;
+        const int diff_scale = c < cn ? 0 : 2;
 
         /* half-sample envelope of the right row over the columns the matches can touch */
         for (int xr = minX2; xr < maxX2; xr++) {
@@ -295,7 +305,7 @@ static int cost_state_init(cost_state* cs, const eff_params* e, int width)
     size_t row = (size_t)e->width1 * e->D;
     cs->hsum = (cost_t*)calloc(row * cs->nrows, sizeof(cost_t));
     cs->pix = (cost_t*)calloc(row, sizeof(cost_t));
-    cs->work = (uint8_t*)calloc((size_t)width * 6, 1);
+    cs->work = (uint8_t*)calloc((size_t)width * (4 * e->cn + 2), 1);
     make_clip_tab(e->ftzero, cs->tab);
     return (cs->hsum && cs->pix && cs->work) ? 0 : -1;
 }
@@ -317,7 +327,7 @@ static void cost_row(cost_state* cs, const uint8_t* L, const uint8_t* R, size_t 
         cost_t* hsumAdd = cs->hsum + (size_t)(imin(k, height - 1) % cs->nrows) * row;
         if (k < height) {
             calc_pixel_cost_bt(L, R, step, width, height, k, e->minD, e->maxD, cs->pix,
-                               cs->tab + TAB_OFS, cs->work);
+                               cs->tab + TAB_OFS, cs->work, e->cn);
             hsum_row(cs->pix, hsumAdd, W1, D, e->SW2);
             if (y > s0) {
                 const cost_t* hsumSub = cs->hsum + (size_t)(imax(y - SH2 - 1, s0) % cs->nrows) * row;
@@ -438,6 +448,101 @@ done:
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* MODE_HH4: computeDisparitySGBM_HH4 (OpenCV 4.x).  4 paths over a full-DP cost buffer:        */
+/*   CalcVerticalSums   -- per column, pass 1 top-to-bottom (C rows formed as in MODE_HH, so the */
+/*                         bottom rows the running sum never reaches keep P2; S cleared), pass 2 */
+/*                         bottom-to-top; each adds its L into S (saturating);                   */
+/*   CalcHorizontalSums -- per row, left-to-right, then right-to-left with the WTA (scalar       */
+/*                         uniqueness, x descending for disp2), then the row's LR check.         */
+/* ------------------------------------------------------------------------------------------ */
+static int sgbm_hh4(const uint8_t* L, const uint8_t* R, int width, int height, size_t step,
+                    const eff_params* e, int16_t* disp, size_t dstride)
+{
+    const int W1 = e->width1, D = e->D, P1 = e->P1, P2 = e->P2;
+    const size_t row = (size_t)W1 * D;
+    const size_t lst = (size_t)D + 2; /* L record with the d = -1 / d = D sentinels */
+    cost_t* Cbuf = (cost_t*)malloc(row * height * sizeof(cost_t));
+    cost_t* Sbuf = (cost_t*)calloc(row * height, sizeof(cost_t));
+    cost_t* Lv = (cost_t*)malloc(2 * (size_t)W1 * lst * sizeof(cost_t)); /* [2][W1][D+2] */
+    int* mv = (int*)malloc(2 * (size_t)W1 * sizeof(int));
+    cost_t* Lh = (cost_t*)malloc(2 * lst * sizeof(cost_t));
+    int16_t* disp2 = (int16_t*)malloc((size_t)width * sizeof(int16_t));
+    int* disp2cost = (int*)malloc((size_t)width * sizeof(int));
+    cost_state cs;
+    int rc = cost_state_init(&cs, e, width);
+    if (!Cbuf || !Sbuf || !Lv || !mv || !Lh || !disp2 || !disp2cost || rc) { rc = -1; goto done; }
+    for (size_t i = 0; i < row * height; i++) Cbuf[i] = (cost_t)P2;
+
+    /* CalcVerticalSums */
+    for (int pass = 1; pass <= 2; pass++) {
+        for (size_t i = 0; i < 2 * (size_t)W1; i++) {
+            cost_t* l = Lv + i * lst;
+            for (size_t d = 0; d < lst; d++) l[d] = 0;
+            l[0] = l[D + 1] = MAX_COST;
+            mv[i] = 0;
+        }
+        int cur = 0;
+        for (int k = 0; k < height; k++) {
+            const int y = pass == 1 ? k : height - 1 - k;
+            cost_t* C = Cbuf + (size_t)y * row;
+            cost_t* S = Sbuf + (size_t)y * row;
+            if (pass == 1) cost_row(&cs, L, R, step, width, height, e, y, 0, C, y == 0 ? C : C - row);
+            for (int x = 0; x < W1; x++) {
+                const cost_t* Lp = Lv + ((size_t)(1 - cur) * W1 + x) * lst + 1;
+                cost_t* Lo = Lv + ((size_t)cur * W1 + x) * lst + 1;
+                mv[cur * W1 + x] = path_step(C + (size_t)x * D, Lp, mv[(1 - cur) * W1 + x], Lo, D, P1, P2);
+                cost_t* Sp = S + (size_t)x * D;
+                for (int d = 0; d < D; d++) Sp[d] = sat16(Sp[d] + Lo[d]);
+            }
+            cur = 1 - cur;
+        }
+    }
+
+    /* CalcHorizontalSums */
+    for (int y = 0; y < height; y++) {
+        const cost_t* C = Cbuf + (size_t)y * row;
+        cost_t* S = Sbuf + (size_t)y * row;
+        int16_t* drow = disp + (size_t)y * dstride;
+        for (int x = 0; x < width; x++) {
+            drow[x] = (int16_t)e->invalid_scaled;
+            disp2[x] = (int16_t)e->invalid_scaled;
+            disp2cost[x] = MAX_COST;
+        }
+        for (int dir = 0; dir < 2; dir++) {
+            for (size_t i = 0; i < 2; i++) {
+                cost_t* l = Lh + i * lst;
+                for (size_t d = 0; d < lst; d++) l[d] = 0;
+                l[0] = l[D + 1] = MAX_COST;
+            }
+            int m = 0, cur = 0;
+            for (int k = 0; k < W1; k++) {
+                const int x = dir == 0 ? k : W1 - 1 - k;
+                cost_t* Lo = Lh + (size_t)cur * lst + 1;
+                m = path_step(C + (size_t)x * D, Lh + (size_t)(1 - cur) * lst + 1, m, Lo, D, P1, P2);
+                cur = 1 - cur;
+                cost_t* Sp = S + (size_t)x * D;
+                for (int d = 0; d < D; d++) Sp[d] = sat16(Sp[d] + Lo[d]);
+                if (dir == 0) continue;
+                int minS, best, d16;
+                if (!wta_pixel(Sp, e, &minS, &best, &d16)) continue;
+                int _x2 = x + e->minX1 - best - e->minD;
+                if (_x2 >= 0 && _x2 < width && disp2cost[_x2] > minS) {
+                    disp2cost[_x2] = minS;
+                    disp2[_x2] = (int16_t)(best + e->minD);
+                }
+                drow[x + e->minX1] = (int16_t)d16;
+            }
+        }
+        lr_check_row(drow, disp2, width, e);
+    }
+    rc = 0;
+done:
+    cost_state_free(&cs);
+    free(Cbuf); free(Sbuf); free(Lv); free(mv); free(Lh); free(disp2); free(disp2cost);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* A.7: computeDisparity3WaySGBM.  OpenCV 4.x fixes nstripes = 4 ("the number of stripes is    */
 /* fixed, disregarding the number of threads/processors, to make the results fully              */
 /* reproducible"); stripe_overlap = (SADWindowSize/2 + 1) + ceil(0.1 * stripe_sz).  Each stripe */
@@ -541,15 +646,19 @@ static int sgbm3way(const uint8_t* L, const uint8_t* R, int width, int height, s
 }
 
 /* ------------------------------------------------------------------------------------------ */
-int orc_sgbm_compute_stages(const uint8_t* left, const uint8_t* right, int width, int height,
-                            size_t stride, const orc_params* p, int16_t* disp,
-                            size_t disp_stride, int stages)
+int orc_sgbm_compute_cn(const uint8_t* left, const uint8_t* right, int width, int height,
+                        size_t stride, int cn, const orc_params* p, int16_t* disp,
+                        size_t disp_stride, int stages)
 {
     eff_params e;
     if (!left || !right || !disp || !p || width <= 0 || height <= 0) return -1;
+    if (cn != 1 && cn != 3) return -1;
     int rc = make_eff(p, width, &e);
     if (rc) return rc;
-    if (p->mode != ORC_MODE_SGBM && p->mode != ORC_MODE_HH && p->mode != ORC_MODE_SGBM_3WAY) return -3;
+    e.cn = cn;
+    if (p->mode != ORC_MODE_SGBM && p->mode != ORC_MODE_HH && p->mode != ORC_MODE_SGBM_3WAY &&
+        p->mode != ORC_MODE_HH4)
+        return -3;
     int16_t* raw = (int16_t*)malloc((size_t)width * height * sizeof(int16_t));
     if (!raw) return -1;
     if (e.width1 <= 0) {
@@ -559,6 +668,8 @@ int orc_sgbm_compute_stages(const uint8_t* left, const uint8_t* right, int width
         return -4; /* OpenCV reads pixDiff[SW2*Da] out of range here */
     } else if (p->mode == ORC_MODE_SGBM_3WAY) {
         rc = sgbm3way(left, right, width, height, stride, p, &e, raw, (size_t)width);
+    } else if (p->mode == ORC_MODE_HH4) {
+        rc = sgbm_hh4(left, right, width, height, stride, &e, raw, (size_t)width);
     } else {
         rc = sgbm_rows(left, right, width, height, stride, p, &e, raw, (size_t)width, NULL);
     }
@@ -578,6 +689,13 @@ int orc_sgbm_compute_stages(const uint8_t* left, const uint8_t* right, int width
     return 0;
 }
 
+int orc_sgbm_compute_stages(const uint8_t* left, const uint8_t* right, int width, int height,
+                            size_t stride, const orc_params* p, int16_t* disp,
+                            size_t disp_stride, int stages)
+{
+    return orc_sgbm_compute_cn(left, right, width, height, stride, 1, p, disp, disp_stride, stages);
+}
+
 int orc_sgbm_compute(const uint8_t* left, const uint8_t* right, int width, int height,
                      size_t stride, const orc_params* p, int16_t* disp, size_t disp_stride)
 {
@@ -585,17 +703,19 @@ int orc_sgbm_compute(const uint8_t* left, const uint8_t* right, int width, int h
                                    ORC_STAGE_MEDIAN | ORC_STAGE_SPECKLE);
 }
 
-int orc_cost_volume(const uint8_t* left, const uint8_t* right, int width, int height,
-                    size_t stride, const orc_params* p, int16_t* out)
+int orc_cost_volume_cn(const uint8_t* left, const uint8_t* right, int width, int height,
+                       size_t stride, int cn, const orc_params* p, int16_t* out)
 {
     eff_params e;
+    if (cn != 1 && cn != 3) return -1;
     int rc = make_eff(p, width, &e);
     if (rc) return rc;
+    e.cn = cn;
     if (e.width1 <= e.SW2) return -4;
     const size_t row = (size_t)e.width1 * e.D;
     cost_state cs;
     if (cost_state_init(&cs, &e, width)) return -1;
-    const int fullDP = p->mode == ORC_MODE_HH;
+    const int fullDP = p->mode == ORC_MODE_HH || p->mode == ORC_MODE_HH4;
     cost_t* C = (cost_t*)malloc(row * sizeof(cost_t));
     for (size_t i = 0; i < row; i++) C[i] = (cost_t)e.P2;
     for (int y = 0; y < height; y++) {
@@ -614,6 +734,12 @@ int orc_cost_volume(const uint8_t* left, const uint8_t* right, int width, int he
     return 0;
 }
 
+int orc_cost_volume(const uint8_t* left, const uint8_t* right, int width, int height,
+                    size_t stride, const orc_params* p, int16_t* out)
+{
+    return orc_cost_volume_cn(left, right, width, height, stride, 1, p, out);
+}
+
 int orc_pixel_cost_row(const uint8_t* left, const uint8_t* right, int width, int height,
                        size_t stride, int y, int minD, int numD, int preFilterCap, int16_t* out)
 {
@@ -622,7 +748,7 @@ int orc_pixel_cost_row(const uint8_t* left, const uint8_t* right, int width, int
     if (imax(maxD, 0) >= width + imin(minD, 0)) return -4;
     uint8_t* work = (uint8_t*)malloc((size_t)width * 6);
     make_clip_tab(imax(preFilterCap, 15) | 1, tab);
-    calc_pixel_cost_bt(left, right, stride, width, height, y, minD, maxD, out, tab + TAB_OFS, work);
+    calc_pixel_cost_bt(left, right, stride, width, height, y, minD, maxD, out, tab + TAB_OFS, work, 1);
     free(work);
     return 0;
 }

@@ -72,11 +72,19 @@ int orc_sgbm_compute_stages(const uint8_t* left, const uint8_t* right, int width
                             size_t stride, const orc_params* p, int16_t* disp,
                             size_t disp_stride_elems, int stages);
 
+/* StereoSGBM::compute on 8-bit images with cn (1 or 3) interleaved channels (calcPixelCostBT's
+ * cn == 3 branch: per-channel Sobel and raw costs summed), stride bytes per row. */
+int orc_sgbm_compute_cn(const uint8_t* left, const uint8_t* right, int width, int height,
+                        size_t stride, int cn, const orc_params* p, int16_t* disp,
+                        size_t disp_stride_elems, int stages);
+
 /* Cost volume C(y, x, d) = P2 + 5x5 (blockSize) box sum of the BT pixel cost, exactly as the
  * SGBM (stripe start s0 = 0) driver forms it, for every row.  mode selects the bottom-row rule
  * (HH keeps the initial P2 on rows the running sum never reaches).  out: [height][width1][D]. */
 int orc_cost_volume(const uint8_t* left, const uint8_t* right, int width, int height,
                     size_t stride, const orc_params* p, int16_t* out);
+int orc_cost_volume_cn(const uint8_t* left, const uint8_t* right, int width, int height,
+                       size_t stride, int cn, const orc_params* p, int16_t* out);
 
 /* One row of Birchfield-Tomasi pixel costs (calcPixelCostBT), out: [width1][D]. */
 int orc_pixel_cost_row(const uint8_t* left, const uint8_t* right, int width, int height,

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("sdr_sgbm_get_stream", _vp, [_vp]),
     ("sdr_sgbm_compute", _i, [_vp, _vp, _vp, _i, _i, _i, _sz, _vp, _sz]),
     ("sdr_sgbm_compute_device", _i, [_vp, _vp, _vp, _i, _i, _sz, _sz, _i, _vp, _sz, _sz]),
+    ("sdr_sgbm_compute_device_cn", _i, [_vp, _vp, _vp, _i, _i, _i, _sz, _sz, _i, _vp, _sz, _sz]),
     ("sdr_host_alloc", _i, [_sz, _c.POINTER(_c.c_void_p)]),
     ("sdr_host_free", _i, [_vp]),
     ("sdr_sgbm_compute_reproject", _i,

@@ -37,14 +37,17 @@ void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st) {
 
 // ------------------------------------------------------------------------------------------
 // A.1 prefilter (x-Sobel clipped to [0, 2*ftzero], raw intensity; cols 0 and W-1 of both
-// channels = tab[0] = ftzero; rows replicate) + half-sample envelopes (calcPixelCostBT).
+// channels = tab[0] = ftzero; rows replicate) + half-sample envelopes (calcPixelCostBT), per
+// channel of an image with pl.cn (1 or 3) interleaved channels: channel c's operands go to the
+// c-th operand set (R planes 3c..3c+2, L words 3c..3c+2 of a pixel).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ Limg,
                                                    const uint8_t* __restrict__ Rimg, size_t stride,
                                                    size_t fstride, int W, int H, int ftzero,
                                                    Planes pl) {
-    extern __shared__ uint64_t q6[];  // [W] 6 bytes per pixel, then the 3 input rows [3][W] bytes
+    extern __shared__ uint64_t q6[];  // [W] 6 bytes per pixel, then the 3 input rows [3][W*cn] bytes
     const int y = blockIdx.x, img = blockIdx.y, f = blockIdx.z;
+    const int cn = pl.cn, WB = W * cn;
     const uint8_t* base = (img ? Rimg : Limg) + (size_t)f * fstride;
     {
         // the row and its neighbours (replicated at the borders) staged in LDS: one coalesced
@@ -53,393 +56,86 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
         const uint8_t* gn = y > 0 ? gr - stride : gr;
         const uint8_t* gs = y < H - 1 ? gr + stride : gr;
         uint8_t* rows = (uint8_t*)(q6 + W);
-        for (int x = threadIdx.x; x < W; x += blockDim.x) {
+        for (int x = threadIdx.x; x < WB; x += blockDim.x) {
             rows[x] = gn[x];
-            rows[W + x] = gr[x];
-            rows[2 * W + x] = gs[x];
+            rows[WB + x] = gr[x];
+            rows[2 * WB + x] = gs[x];
         }
         __syncthreads();
     }
     const uint8_t* n = (const uint8_t*)(q6 + W);
-    const uint8_t* r = n + W;
-    const uint8_t* s = r + W;
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        int sv[3], rv[3];
+    const uint8_t* r = n + WB;
+    const uint8_t* s = r + WB;
+    const size_t plane = (size_t)H * W;
+    for (int ch = 0; ch < cn; ch++) {
+        for (int x = threadIdx.x; x < W; x += blockDim.x) {
+            int sv[3], rv[3];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            int xx = x + k - 1;
-            if (xx <= 0 || xx >= W - 1) {
-                sv[k] = ftzero;
-                rv[k] = ftzero;
+            for (int k = 0; k < 3; k++) {
+                int xx = x + k - 1;
+                if (xx <= 0 || xx >= W - 1) {
+                    sv[k] = ftzero;
+                    rv[k] = ftzero;
+                } else {
+                    const int a = (xx + 1) * cn + ch, b = (xx - 1) * cn + ch;
+                    int gr = 2 * (r[a] - r[b]) + n[a] - n[b] + s[a] - s[b];
+                    gr = gr < -ftzero ? -ftzero : (gr > ftzero ? ftzero : gr);
+                    sv[k] = gr + ftzero;
+                    rv[k] = r[xx * cn + ch];
+                }
+            }
+            uint64_t q = 0;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int* val = c == 0 ? sv : rv;
+                int v = val[1];
+                int a = x < W - 1 ? (v + val[2]) >> 1 : v;
+                int b = x > 0 ? (v + val[0]) >> 1 : v;
+                int lo = min(min(a, b), v), hi = max(max(a, b), v);
+                q |= (uint64_t)v << (24 * c);
+                q |= (uint64_t)lo << (24 * c + 8);
+                q |= (uint64_t)hi << (24 * c + 16);
+            }
+            q6[x] = q;
+        }
+        __syncthreads();
+        for (int x = threadIdx.x; x < W; x += blockDim.x) {
+            const uint64_t a = q6[x];
+            const uint64_t b = q6[x > 0 ? x - 1 : 0];
+            uint32_t w[6];
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                const uint32_t va = (uint32_t)(a >> (8 * c)) & 0xff, vb = (uint32_t)(b >> (8 * c)) & 0xff;
+                w[c] = img ? (va | (vb << 16)) : va * 0x10001u;
+            }
+            if (img) {
+                uint64_t* dst = pl.R + (size_t)f * pl.fstrideR + 3 * ch * plane + (size_t)y * W + x;
+                dst[0] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+                dst[plane] = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+                dst[2 * plane] = (uint64_t)w[4] | ((uint64_t)w[5] << 32);
             } else {
-                int gr = 2 * (r[xx + 1] - r[xx - 1]) + n[xx + 1] - n[xx - 1] + s[xx + 1] - s[xx - 1];
-                gr = gr < -ftzero ? -ftzero : (gr > ftzero ? ftzero : gr);
-                sv[k] = gr + ftzero;
-                rv[k] = r[xx];
+                // one 12-byte store per pixel and channel (gray: a wave writes 768 contiguous bytes)
+                typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+                const u32x3 v = {(w[0] & 0xffffu) | (w[1] << 16), (w[2] & 0xffffu) | (w[3] << 16),
+                                 (w[4] & 0xffffu) | (w[5] << 16)};
+                *(u32x3*)(pl.L + (size_t)f * pl.fstrideL + ((size_t)y * W + x) * 3 * cn + 3 * ch) = v;
             }
         }
-        uint64_t q = 0;
-#pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const int* val = c == 0 ? sv : rv;
-            int v = val[1];
-            int a = x < W - 1 ? (v + val[2]) >> 1 : v;
-            int b = x > 0 ? (v + val[0]) >> 1 : v;
-            int lo = min(min(a, b), v), hi = max(max(a, b), v);
-            q |= (uint64_t)v << (24 * c);
-            q |= (uint64_t)lo << (24 * c + 8);
-            q |= (uint64_t)hi << (24 * c + 16);
-        }
-        q6[x] = q;
-    }
-    __syncthreads();
-    const size_t plane = (size_t)H * W;
-    for (int x = threadIdx.x; x < W; x += blockDim.x) {
-        const uint64_t a = q6[x];
-        const uint64_t b = q6[x > 0 ? x - 1 : 0];
-        uint32_t w[6];
-#pragma unroll
-        for (int c = 0; c < 6; c++) {
-            const uint32_t va = (uint32_t)(a >> (8 * c)) & 0xff, vb = (uint32_t)(b >> (8 * c)) & 0xff;
-            w[c] = img ? (va | (vb << 16)) : va * 0x10001u;
-        }
-        if (img) {
-            uint64_t* dst = pl.R + (size_t)f * pl.fstrideR + (size_t)y * W + x;
-            dst[0] = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-            dst[plane] = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
-            dst[2 * plane] = (uint64_t)w[4] | ((uint64_t)w[5] << 32);
-        } else {
-            // one 12-byte store per pixel (a wave writes 768 contiguous bytes in one instruction)
-            typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-            const u32x3 v = {(w[0] & 0xffffu) | (w[1] << 16), (w[2] & 0xffffu) | (w[3] << 16),
-                             (w[4] & 0xffffu) | (w[5] << 16)};
-            *(u32x3*)(pl.L + (size_t)f * pl.fstrideL + ((size_t)y * W + x) * 3) = v;
-        }
+        if (ch + 1 < cn) __syncthreads();  // q6 is rewritten by the next channel
     }
 }
 
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
                       int H, int F, int ftzero, const Planes& pl, hipStream_t st) {
-    hipLaunchKernelGGL(k_prefilter, dim3(H, 2, F), dim3(256), (size_t)W * 11, st, L, R, stride, fstride,
-                       W, H, ftzero, pl);
+    hipLaunchKernelGGL(k_prefilter, dim3(H, 2, F), dim3(256), (size_t)W * (8 + 3 * pl.cn), st, L, R,
+                       stride, fstride, W, H, ftzero, pl);
 }
 
-// ------------------------------------------------------------------------------------------
-// A.2 + A.3 cost volume
-//   C(y, x, d) = P2 + sum_{|j|<=SH2} hsum(clamp(t(y)+j, s0, H-1), x, d),   t(y) = min(y, ylim)
-//   hsum(r, x, d) = sum_{|k|<=SW2} BT(r, clamp(x+k, 0, W1-1), d)
-// equals OpenCV's running sums in int16 wrap arithmetic, incl. the bottom rows where the running
-// sum stops updating (t clamps at ylim = H-1-SH2) and MODE_HH's untouched P2 rows.  The sums are
-// taken in the other order here, vertical first (V(x) = sum over the window's rows of BT(x)),
-// then horizontal over the V of the clamped columns: the same int16 wrap sum.
-// The window is walked over "virtual" rows q = t-SH2 .. t+SH2 (physical row clamp(q, s0, H-1)),
-// so the ring of the last NR rows is a plain sliding window with compile-time slots.
-// ------------------------------------------------------------------------------------------
-// parity half of a staged R plane: >= ceil(STR/2), == 16 (mod 32) so the even/odd halves of a
-// 32-lane staging store land on disjoint banks
-__host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 15) / 32 * 32 + 16; }
+}  // namespace sdr
 
-template <int NR, int K>
-struct CostCfg {
-    static constexpr int SW2 = (NR - 1) / 2;
-    static constexpr int BCOLS = K == 1 ? 32 : 16;  // output columns of a block
-    static constexpr int CW = BCOLS / 4;            // output columns per wave (horizontal sums)
-    static constexpr int NPB = BCOLS + 2 * SW2;     // pixel-cost columns the block needs
-    static constexpr int PCW = (NPB + 3) / 4;       // pixel-cost columns per wave: p = wave + 4*jj
-    static constexpr int NLV = 4 * PCW;             // staged virtual columns
-    // row prefetch depth and the row loop's unroll: U covers the ring slot (% NR), the LDS
-    // double buffer (% 2) and the prefetch register slot (% PD) statically
-    // (two rows: deeper prefetch costs registers, i.e. resident blocks, and measured slower)
-    static constexpr int PD = 2;
-    static constexpr int U = 2 * NR;
-    // LDS bytes: two staging buffers (R: 3 pair planes x 2 parity halves, L: 4 words a column)
-    // + two column-sum buffers
-    static size_t lds_bytes(int D) {
-        return (size_t)2 * 6 * cost_half_r(NLV + D) * 8 + (size_t)2 * NLV * 16 + (size_t)2 * NLV * K * 64 * 4;
-    }
-};
+#include "sdr_cost_kernel.hpp"
 
-// Birchfield-Tomasi dissimilarity of packed pairs: min(max(0, u-v1, v0-u), max(0, v-u1, u0-v)).
-// Operands are in [0, 255], so max(x, 0) of a difference is an unsigned saturating subtract and
-// one of each pair is zero: 4 v_pk_sub_u16 (clamp) + 2 v_pk_max_u16 + 1 v_pk_min_u16.
-__device__ __forceinline__ uint32_t bt_cost(uint32_t u, uint32_t u0, uint32_t u1, uint32_t v,
-                                            uint32_t v0, uint32_t v1) {
-    const uint32_t c0 = pk_max_u(pk_sub_usat(u, v1), pk_sub_usat(v0, u));
-    const uint32_t c1 = pk_max_u(pk_sub_usat(v, u1), pk_sub_usat(u0, v));
-    return pk_min_u(c0, c1);
-}
-// a 16-bit half of a word broadcast to both halves: folds into the packed op as an op_sel
-// operand selection
-__device__ __forceinline__ uint32_t half_lo(uint32_t w) {
-    const u16x2 v = as_u16x2(w);
-    return as_u32(__builtin_shufflevector(v, v, 0, 0));
-}
-__device__ __forceinline__ uint32_t half_hi(uint32_t w) {
-    const u16x2 v = as_u16x2(w);
-    return as_u32(__builtin_shufflevector(v, v, 1, 1));
-}
-
-template <int NR, int K, bool EDGE>
-__device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a, uint64_t* lds,
-                                           int bx, int f, int ty0, int ty1) {
-    using Cfg = CostCfg<NR, K>;
-    constexpr int SW2 = Cfg::SW2, SH2 = SW2, BCOLS = Cfg::BCOLS, CW = Cfg::CW;
-    constexpr int PCW = Cfg::PCW, NLV = Cfg::NLV, PD = Cfg::PD, U = Cfg::U;
-    static_assert(U % PD == 0 && U % NR == 0 && U % 2 == 0, "static slots");
-    const int W = g.W, H = g.H, W1 = g.W1, D = g.D;
-    const int lane = threadIdx.x & 63, tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int bx0 = bx * BCOLS;
-    const uint32_t P2x2 = splat16(g.P2);
-    int16_t* out = a.out + (size_t)f * a.out_fstride;
-
-    // output addressing: the wave's first row and column in a buffer resource, rows and columns
-    // as scalar offsets, the lane's pair as the one vector offset.  Lanes past the last
-    // disparity pair alias it (they compute and store the same value to the same word), so every
-    // store is unconditional and the number of stores per row is static: hipcc then counts the
-    // outstanding stores exactly and does not wait for the row prefetches behind them.
-    const int ox0 = bx0 + wave * CW;
-    const int ncols = EDGE ? min(CW, W1 - ox0) : CW;
-    const uint32_t colb = (uint32_t)D * 2, rowb = (uint32_t)W1 * colb;
-    const Rsrc rO = rsrc_at(out + ((size_t)(ty0 - a.out_row0) * W1 + ox0) * D);
-    const Rsrc rSink = rsrc_at(a.sink + (size_t)ox0 * D);
-    int qpc[K];
-    uint32_t vo[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        qpc[i] = min(lane + 64 * i, D / 2 - 1);
-        vo[i] = 4 * qpc[i];
-    }
-    auto emit_at = [&](Rsrc r, uint32_t so, auto&& val) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < K; i++)
-#pragma unroll
-            for (int c = 0; c < CW; c++)
-                if (!EDGE || c < ncols) __builtin_amdgcn_raw_buffer_store_b32(val(i, c), r, vo[i], so + c * colb, 0);
-    };
-    auto emit = [&](int y, auto&& val) __attribute__((always_inline)) { emit_at(rO, (uint32_t)(y - ty0) * rowb, val); };
-
-    // rows [yl, ty1) of MODE_HH keep the initial P2
-    int yl = ty1;
-    if (a.hh_bottom) yl = max(ty0, min(ty1, max(1, H - SH2)));
-    for (int y = yl; y < ty1; y++) emit(y, [&](int, int) { return P2x2; });
-    if (yl <= ty0) return;
-
-    // Virtual columns v = vlo + p, p = 0 .. NLV-1; wave w computes the pixel costs of columns
-    // p = w + 4*jj.  Left operands are staged for image columns minX1 + clamp(v, 0, W1-1); R pairs
-    // for xr = minX1 + vlo - minD - (D-2) + e, e = 0 .. NLV+D-3: the pair of disparities
-    // (2qp, 2qp+1) of column p sits at e = p + D-2 - 2qp.  Columns beyond [0, W1) are computed
-    // from clamped data and never read: the horizontal sums read the column sums of clamp(v),
-    // which is what x clamping means.
-    const int vlo = bx0 - SW2;
-    const int NRP = NLV + D - 2;
-    const int HR = cost_half_r(NLV + D);  // entries per parity half of a staged R plane
-    const int BUFR = 6 * HR;
-    uint32_t* LB = (uint32_t*)(lds + 2 * BUFR);  // [2][NLV][4] left operand words
-    uint32_t* VB = LB + 2 * NLV * 4;             // [2][NLV][K][64] column sums
-    const uint32_t planeb = (uint32_t)H * W * 8;
-
-    // ---- staging: a row of the R pair planes and of the L pack, global -> registers -> LDS ----
-    // Rows are fetched PD rows ahead into PD register slots (slot of row r: (r - qbeg) % PD), so
-    // a load has PD row steps to land.  Loads are unconditional with clamped indices and
-    // rows (surplus lanes re-load and re-store the last entry, the same value to the same slot):
-    // a guarded load makes hipcc branch around it and wait vmcnt(0) right after it is issued.
-    // Staging goes through registers, not LDS-direct loads, because the barrier of every row
-    // would then wait for all of them.
-    constexpr int NPR = K;  // R entries per thread per plane: NRP <= 256 * K
-    const int xr0 = g.minX1 + vlo - g.minD - (D - 2);
-    const Rsrc rR = rsrc_at(a.pl.R + (size_t)f * a.pl.fstrideR);  // < 2 GiB a frame (check_frame)
-    const Rsrc rL = rsrc_at(a.pl.L + (size_t)f * a.pl.fstrideL);
-    uint32_t gr[NPR];
-    int pr[NPR];
-#pragma unroll
-    for (int t = 0; t < NPR; t++) {
-        const int ir = min(tid + 256 * t, NRP - 1);
-        gr[t] = 8 * min(max(xr0 + ir, 0), W - 1);
-        pr[t] = (ir & 1) * HR + (ir >> 1);
-    }
-    const int il = min(tid, 3 * NLV - 1);  // L word il: column il / 3, word il % 3
-    const uint32_t gl = 4 * (3 * (g.minX1 + min(max(vlo + il / 3, 0), W1 - 1)) + il % 3);
-    const int pl = (il / 3) * 4 + il % 3;
-    struct Stage {
-        uint64_t r[3][NPR];
-        uint32_t l;
-    };
-    Stage st[PD];
-    auto fetch = [&](int r, Stage& sg) __attribute__((always_inline)) {
-        const uint32_t so = (uint32_t)r * W * 8;
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-#pragma unroll
-            for (int t = 0; t < NPR; t++) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rR, gr[t], so + k * planeb, 0);
-                sg.r[k][t] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
-            }
-        sg.l = __builtin_amdgcn_raw_buffer_load_b32(rL, gl, (uint32_t)r * W * 12, 0);
-    };
-    auto put = [&](int b, const Stage& sg) __attribute__((always_inline)) {
-        uint64_t* BR = lds + b * BUFR;
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-#pragma unroll
-            for (int t = 0; t < NPR; t++) BR[k * 2 * HR + pr[t]] = sg.r[k][t];
-        LB[b * NLV * 4 + pl] = sg.l;
-    };
-
-    // per-lane staged R position of this wave's column jj: (p & 1) * HR + p / 2 + (D-2)/2 - qp
-    // with p = wave + 4*jj, i.e. rpos + 2*jj
-    int rpos[K];
-#pragma unroll
-    for (int i = 0; i < K; i++) rpos[i] = (wave & 1) * HR + (wave >> 1) + (D - 2) / 2 - qpc[i];
-    // column sums: written at [p][i][lane], read back for columns clamp(wave*CW + c', plo, phi)
-    uint32_t* Vw = VB + (wave * K) * 64 + lane;
-    const int plo = SW2 - bx0, phi = W1 - 1 - vlo;
-
-    // virtual rows and outputs
-    const int ylim = a.ylim, s0 = a.s0;
-    const int tfirst = min(ty0, ylim), tlast = min(yl - 1, ylim);
-    const int qbeg = tfirst - SH2, qend = tlast + SH2;
-    auto phys = [&](int q) { return min(max(min(q, qend), s0), H - 1); };
-
-    // horizontal sums (+ P2) of the column sums in buffer b
-    auto hsum = [&](int b, uint32_t (&hs)[K][CW]) __attribute__((always_inline)) {
-        const uint32_t* V = VB + b * (NLV * K * 64) + (wave * CW) * K * 64 + lane;
-#pragma unroll
-        for (int i = 0; i < K; i++) {
-            uint32_t v[CW + 2 * SW2];
-#pragma unroll
-            for (int c = 0; c < CW + 2 * SW2; c++) {
-                int dc = c;  // interior: immediate offsets from one base
-                if (EDGE) dc = min(max(wave * CW + c, plo), phi) - wave * CW;
-                v[c] = V[(dc * K + i) * 64];
-            }
-            uint32_t h = P2x2;
-#pragma unroll
-            for (int k = 0; k < 2 * SW2 + 1; k++) h = pk_add(h, v[k]);
-            hs[i][0] = h;
-#pragma unroll
-            for (int c = 1; c < CW; c++) {
-                h = pk_sub(pk_add(h, v[c + 2 * SW2]), v[c - 1]);
-                hs[i][c] = h;
-            }
-        }
-    };
-
-    uint32_t ring[NR][K][PCW], vs[K][PCW];
-#pragma unroll
-    for (int s = 0; s < NR; s++)
-#pragma unroll
-        for (int i = 0; i < K; i++)
-#pragma unroll
-            for (int jj = 0; jj < PCW; jj++) ring[s][i][jj] = 0;
-#pragma unroll
-    for (int i = 0; i < K; i++)
-#pragma unroll
-        for (int jj = 0; jj < PCW; jj++) vs[i][jj] = 0;
-
-    fetch(phys(qbeg), st[0]);
-    put(0, st[0]);
-#pragma unroll
-    for (int k = 1; k <= PD; k++) fetch(phys(qbeg + k), st[k % PD]);
-    __syncthreads();
-
-    // one barrier per virtual row q = qbeg + j (mod U): (A) horizontal sums + outputs of the
-    // column sums row q-1 left in LDS, (B) staging of row q+1 and the fetch of row q+1+PD, (C)
-    // pixel costs of row q, the vertical window, its column sums into LDS
-    auto row = [&](const int q, auto jc) __attribute__((always_inline)) {
-        constexpr int j = decltype(jc)::value;
-        constexpr int s = j % NR, b = j & 1;
-        {
-            // output row t = q-1-SH2 < tlast; rows before ty0 (the window's warm-up, or a band in
-            // the frozen bottom rows) go to the sink row instead of a branch around the stores
-            uint32_t hs[K][CW];
-            hsum(b ^ 1, hs);
-            const int t = q - 1 - SH2;
-            const bool real = t >= ty0;
-            emit_at(real ? rO : rSink, real ? (uint32_t)(t - ty0) * rowb : 0u, [&](int i, int c) { return hs[i][c]; });
-        }
-        put((j + 1) & 1, st[(j + 1) % PD]);
-        fetch(phys(q + 1 + PD), st[(j + 1) % PD]);
-        const uint64_t* BR = lds + b * BUFR;
-        const uint32_t* BL = LB + b * NLV * 4 + wave * 4;
-#pragma unroll
-        for (int jj = 0; jj < PCW; jj++) {
-            // a broadcast read: every lane reads the column's three words
-            const uint32_t w0 = BL[16 * jj], w1 = BL[16 * jj + 1], w2 = BL[16 * jj + 2];
-            const uint32_t u = half_lo(w0), u0 = half_hi(w0), u1 = half_lo(w1);
-            const uint32_t ur = half_hi(w1), ur0 = half_lo(w2), ur1 = half_hi(w2);
-#pragma unroll
-            for (int i = 0; i < K; i++) {
-                const uint64_t* BRj = BR + rpos[i] + 2 * jj;
-                const uint64_t r0 = BRj[0], r1 = BRj[2 * HR], r2 = BRj[4 * HR];
-                const uint32_t bs = bt_cost(u, u0, u1, (uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1);
-                const uint32_t br = bt_cost(ur, ur0, ur1, (uint32_t)(r1 >> 32), (uint32_t)r2, (uint32_t)(r2 >> 32));
-                const uint32_t pix = pk_add(bs, pk_shr2_u(br));
-                vs[i][jj] = pk_sub(pk_add(vs[i][jj], pix), ring[s][i][jj]);
-                ring[s][i][jj] = pix;
-            }
-        }
-        {
-            // (partial sums during the warm-up: their horizontal sums go to the sink)
-            uint32_t* Vb = Vw + b * (NLV * K * 64);
-#pragma unroll
-            for (int jj = 0; jj < PCW; jj++)
-#pragma unroll
-                for (int i = 0; i < K; i++) Vb[(4 * jj * K + i) * 64] = vs[i][jj];
-        }
-        __syncthreads();
-    };
-    int qq = qbeg;
-    for (; qq + U - 1 <= qend; qq += U) unroll_rows(row, qq, std::make_integer_sequence<int, U>{});
-    unroll_rows_tail(row, qq, qend, std::make_integer_sequence<int, U>{});
-    // the last window, t = tlast: its rows [max(tlast, ty0), yl) (the frozen bottom rows repeat it)
-    uint32_t hs[K][CW];
-    hsum((qend - qbeg) & 1, hs);
-    for (int y = max(tlast, ty0); y < yl; y++) emit(y, [&](int i, int c) { return hs[i][c]; });
-}
-
-template <int NR, int K>
-__global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
-    using Cfg = CostCfg<NR, K>;
-    extern __shared__ uint64_t lds[];
-    // column blocks of one row band are consecutive logical blocks: they share an XCD, so the
-    // right-image rows they all stage (each block reads D-2 columns of halo) are re-read from L2
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int l = xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
-    const int bx = l % gx, by = (l / gx) % gy, f = l / (gx * gy);
-    const int ty0 = a.row_begin + by * a.TY;
-    const int ty1 = min(ty0 + a.TY, a.row_end);
-    if (ty0 >= ty1) return;
-    const int bx0 = bx * Cfg::BCOLS;
-    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, true>(g, a, lds, bx, f, ty0, ty1);
-    else cost_block<NR, K, false>(g, a, lds, bx, f, ty0, ty1);
-}
-
-template <int NR, int K>
-static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) {
-    using Cfg = CostCfg<NR, K>;
-    const int rows = a.row_end - a.row_begin;
-    const size_t lds = Cfg::lds_bytes(g.D);
-    const int colblocks = (g.W1 + Cfg::BCOLS - 1) / Cfg::BCOLS;
-    if (a.TY <= 0) {
-        // one full pass of resident blocks: a partial second pass doubles the kernel time, and
-        // each block re-walks NR-1 warm-up rows, so use the tallest row band that fills the chip
-        static thread_local size_t key = 0;
-        static thread_local int slots = 0;
-        if (key != lds) {
-            int dev = 0, cus = 0, per_cu = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_cost<NR, K>, 256, lds);
-            slots = max(1, cus * max(1, per_cu));
-            key = lds;
-        }
-        const int bands = max(1, slots / max(1, colblocks * F));
-        a.TY = max(4, (rows + bands - 1) / bands);
-    }
-    dim3 grid(colblocks, (rows + a.TY - 1) / a.TY, F);
-    hipLaunchKernelGGL((k_cost<NR, K>), grid, dim3(256), lds, st, g, a);
-}
+namespace sdr {
 
 // one output row of the widest column-block span (racing garbage from every block)
 size_t cost_sink_bytes(const Geometry& g) { return (size_t)(g.W1 + 64) * g.D * 2; }
@@ -448,12 +144,13 @@ bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.SH2 <= 5 && 
 
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st) {
     if (a.row_end <= a.row_begin) return;
+    if (a.pl.cn == 3) return launch_cost_cn3(g, a, F, st);
     const int NR = 2 * g.SH2 + 1;
     const bool k2 = g.D > 128;
 #define SDR_COST(NRV)                                                 \
     case NRV:                                                         \
-        if (k2) launch_cost_t<NRV, 2>(g, a, F, st);                   \
-        else launch_cost_t<NRV, 1>(g, a, F, st);                      \
+        if (k2) launch_cost_t<NRV, 2, 1>(g, a, F, st);                \
+        else launch_cost_t<NRV, 1, 1>(g, a, F, st);                   \
         break;
     switch (NR) {
         SDR_COST(1) SDR_COST(3) SDR_COST(5) SDR_COST(7) SDR_COST(9) SDR_COST(11)

@@ -48,8 +48,9 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     if (p.numDisparities <= 0 || p.numDisparities % 16 != 0)
         return fail(SDR_ERR_NUMDISP, "numDisparities must be positive and divisible by 16");
     if (p.numDisparities > 256) return fail(SDR_ERR_LIMIT, "numDisparities > 256 is not supported");
-    if (p.mode != SDR_MODE_SGBM && p.mode != SDR_MODE_HH && p.mode != SDR_MODE_SGBM_3WAY)
-        return fail(SDR_ERR_MODE, "unsupported mode (MODE_HH4 is not implemented)");
+    if (p.mode != SDR_MODE_SGBM && p.mode != SDR_MODE_HH && p.mode != SDR_MODE_SGBM_3WAY &&
+        p.mode != SDR_MODE_HH4)
+        return fail(SDR_ERR_MODE, "unknown mode");
     sdr::Geometry& g = e->g;
     g.W = W;
     g.H = H;
@@ -111,6 +112,21 @@ int check_frame(const Eff& e) {
     if ((size_t)g.H * g.W * 24 > (size_t)INT32_MAX)
         return fail(SDR_ERR_SIZE, "frame too large: the right image's cost planes span more than 2 GiB");
     if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
+    return SDR_OK;
+}
+
+// Channel count of the input pair (OpenCV: CV_8UC1 or CV_8UC3; calcPixelCostBT's cn == 3 branch
+// sums each channel's Sobel and raw costs, so the int16 domain bound grows with it).
+int check_channels(const Eff& e, int cn) {
+    if (cn != 1 && cn != 3) return fail(SDR_ERR_TYPE, "images must have 1 or 3 channels");
+    if (cn == 1) return SDR_OK;
+    const sdr::Geometry& g = e.g;
+    const long bmax = (long)cn * (2 * e.ftzero + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
+    if (2L * g.P2 + bmax > 32767)
+        return fail(SDR_ERR_LIMIT, "2*P2 + 3*(2*preFilterCap+63)*blockSize^2 exceeds the int16 cost "
+                                   "range (OpenCV's SIMD and scalar builds disagree there)");
+    if ((size_t)g.H * g.W * 24 * cn > (size_t)INT32_MAX)
+        return fail(SDR_ERR_SIZE, "frame too large: the right image's cost planes span more than 2 GiB");
     return SDR_OK;
 }
 
@@ -374,7 +390,9 @@ static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
                         px * 4 * 2);
 }
 
-static int npaths_of(int mode) { return mode == SDR_MODE_HH ? 8 : mode == SDR_MODE_SGBM ? 5 : 3; }
+static int npaths_of(int mode) {
+    return mode == SDR_MODE_HH ? 8 : mode == SDR_MODE_SGBM ? 5 : mode == SDR_MODE_HH4 ? 4 : 3;
+}
 
 // Enqueues the full compute for F frames whose inputs are already on the device.
 //   prefilter -> cost volume (+ 3WAY stripe-start rows) -> the P-1 directions other than
@@ -386,10 +404,11 @@ static int npaths_of(int mode) { return mode == SDR_MODE_HH ? 8 : mode == SDR_MO
 //   out_min (nullable): per-frame minimum of the final map (reprojectImageTo3D handleMissing)
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
-                           int16_t** final_disp) {
+                           int16_t** final_disp, int cn = 1) {
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
+    if ((rc = check_channels(e, cn))) return rc;
     const sdr::Geometry& g = e.g;
     hipStream_t st = h->stream;
     const size_t px = (size_t)W * H;
@@ -413,8 +432,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     for (auto& s : stripes) amax = std::max(amax, s.aux_rows);
     const size_t aux_fstride = (size_t)stripes.size() * amax * g.W1 * g.D;
 
-    if ((rc = ensure(h->planesL, F * 3 * px * 4))) return rc;
-    if ((rc = ensure(h->planesR, F * 3 * px * 8))) return rc;
+    if ((rc = ensure(h->planesL, F * 3 * px * 4 * cn))) return rc;
+    if ((rc = ensure(h->planesR, F * 3 * px * 8 * cn))) return rc;
     if ((rc = ensure(h->sink, sdr::cost_sink_bytes(g)))) return rc;
     // the path kernels' loads overrun a chain's ends by up to kSouthPad rows: slack both sides
     const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
@@ -443,7 +462,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     sdr::Planes pl;
     pl.L = (uint32_t*)h->planesL.p;
     pl.R = (uint64_t*)h->planesR.p;
-    pl.fstrideL = pl.fstrideR = 3 * px;
+    pl.fstrideL = pl.fstrideR = 3 * px * cn;
+    pl.cn = cn;
     { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st); }
 
     sdr::CostArgs ca{};
@@ -455,7 +475,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     ca.row_end = H;
     ca.s0 = 0;
     ca.ylim = std::max(H - 1 - g.SH2, 0);
-    ca.hh_bottom = e.mode == SDR_MODE_HH;
+    // the full-DP cost buffers of MODE_HH and MODE_HH4 keep P2 on the rows the running sum never reaches
+    ca.hh_bottom = e.mode == SDR_MODE_HH || e.mode == SDR_MODE_HH4;
     ca.TY = 0;  // sized by launch_cost for one full pass of resident blocks
     ca.sink = (int16_t*)h->sink.p;
     { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
@@ -516,6 +537,10 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
                 d.aux_rows = sp.aux_rows;
             }
         }
+    } else if (e.mode == SDR_MODE_HH4) {
+        // computeDisparitySGBM_HH4: the two vertical and the two horizontal directions
+        add_dir(plS, sdr::DIR_S, nS, nullptr);
+        add_dir(pls, sdr::DIR_N, nS, buf());
     } else {
         add_dir(plS, sdr::DIR_S, nS, nullptr);
         if (e.mode == SDR_MODE_HH) add_dir(pls, sdr::DIR_N, nS, buf());
@@ -705,8 +730,16 @@ static int check_dims(int W, int H, size_t stride, int F) {
 int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, int W, int H,
                             size_t stride, size_t fstride, int F, int16_t* dDisp,
                             size_t disp_stride, size_t disp_fstride) {
+    return sdr_sgbm_compute_device_cn(h, dL, dR, W, H, 1, stride, fstride, F, dDisp, disp_stride,
+                                      disp_fstride);
+}
+
+int sdr_sgbm_compute_device_cn(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, int W, int H,
+                               int channels, size_t stride, size_t fstride, int F, int16_t* dDisp,
+                               size_t disp_stride, size_t disp_fstride) {
     if (!h || !dL || !dR || !dDisp) return fail(SDR_ERR_ARG, "null argument");
-    int rc = check_dims(W, H, stride, F);
+    if (channels != 1 && channels != 3) return fail(SDR_ERR_TYPE, "images must have 1 or 3 channels");
+    int rc = check_dims(W * channels, H, stride, F);
     if (rc) return rc;
     if (disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
     if (F > 1 && fstride < stride * H) return fail(SDR_ERR_ARG, "frame_stride too small");
@@ -714,7 +747,8 @@ int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR, i
     int16_t* fin = nullptr;
     const size_t px = (size_t)W * H;
     const bool dense = disp_stride == (size_t)W && (F == 1 || disp_fstride == px);
-    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, dense ? dDisp : nullptr, nullptr, &fin)))
+    if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, dense ? dDisp : nullptr, nullptr, &fin,
+                              channels)))
         return rc;
     if (!dense) {
         for (int f = 0; f < F; f++)
@@ -735,7 +769,7 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint
     SDR_HIP(hipSetDevice(h->device));
     int16_t* fin = nullptr;
     const size_t px = (size_t)W * H;
-    if ((rc = ensure(h->mins, (size_t)F * 4))) return rc;
+    if ((rc = ensure(h->mins, (size_t)F * 4 * sdr::kMinSlots))) return rc;
     int* mins = handle_missing ? (int*)h->mins.p : nullptr;
     if ((rc = enqueue_compute(h, dL, dR, W, H, stride, fstride, F, dDisp, mins, &fin))) return rc;
     {
@@ -751,20 +785,21 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint
 int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int W, int H,
                      int channels, size_t stride, int16_t* disp, size_t disp_stride) {
     if (!h || !left || !right || !disp) return fail(SDR_ERR_ARG, "null argument");
-    if (channels != 1) return fail(SDR_ERR_TYPE, "only 8-bit single-channel images are supported");
-    int rc = check_dims(W, H, stride, 1);
+    if (channels != 1 && channels != 3) return fail(SDR_ERR_TYPE, "images must have 1 or 3 channels");
+    const int cn = channels;
+    int rc = check_dims(W * cn, H, stride, 1);
     if (rc) return rc;
     if (disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
     SDR_HIP(hipSetDevice(h->device));
-    const size_t px = (size_t)W * H;
-    if ((rc = ensure(h->hin, 2 * px))) return rc;
-    if ((rc = h->hx.begin(2 * stage_bytes(px) + stage_bytes(px * 2)))) return rc;
+    const size_t px = (size_t)W * H, ib = px * cn;
+    if ((rc = ensure(h->hin, 2 * ib))) return rc;
+    if ((rc = h->hx.begin(2 * stage_bytes(ib) + stage_bytes(px * 2)))) return rc;
     uint8_t* dL = (uint8_t*)h->hin.p;
-    uint8_t* dR = dL + px;
-    if ((rc = h->hx.upload(dL, W, left, stride, W, H, h->stream))) return rc;
-    if ((rc = h->hx.upload(dR, W, right, stride, W, H, h->stream))) return rc;
+    uint8_t* dR = dL + ib;
+    if ((rc = h->hx.upload(dL, (size_t)W * cn, left, stride, (size_t)W * cn, H, h->stream))) return rc;
+    if ((rc = h->hx.upload(dR, (size_t)W * cn, right, stride, (size_t)W * cn, H, h->stream))) return rc;
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, nullptr, &fin))) return rc;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, (size_t)W * cn, ib, 1, nullptr, nullptr, &fin, cn))) return rc;
     if ((rc = h->hx.download(disp, disp_stride * 2, fin, (size_t)W * 2, (size_t)W * 2, H, h->stream))) return rc;
     return h->hx.drain();
 }
@@ -781,7 +816,7 @@ int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* 
     const size_t px = (size_t)W * H;
     if ((rc = ensure(h->hin, 2 * px))) return rc;
     if ((rc = ensure(h->hxyz, px * 12))) return rc;
-    if ((rc = ensure(h->mins, 4))) return rc;
+    if ((rc = ensure(h->mins, 4 * sdr::kMinSlots))) return rc;
     if ((rc = h->hx.begin(2 * stage_bytes(px) + stage_bytes(px * 2) + stage_bytes(px * 12)))) return rc;
     uint8_t* dL = (uint8_t*)h->hin.p;
     uint8_t* dR = dL + px;
@@ -851,7 +886,7 @@ int sdr_disp16_reproject_device(const int16_t* d_disp, int W, int H, size_t disp
     int* mins = nullptr;
     hipStream_t st = (hipStream_t)stream;
     if (handle_missing) {
-        SDR_HIP(hipMallocAsync((void**)&mins, F * sizeof(int), st));
+        SDR_HIP(hipMallocAsync((void**)&mins, F * sdr::kMinSlots * sizeof(int), st));
         sdr::launch_min_s16(d_disp, (size_t)W * H, disp_stride * H, F, mins, st);
     }
     sdr::launch_reproject_s16(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,

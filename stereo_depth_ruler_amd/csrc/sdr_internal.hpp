@@ -8,6 +8,11 @@
 
 namespace sdr {
 
+// partial per-frame minima of the int16 disparity (launch_min_s16 / launch_speckle's out_min):
+// [F][kMinSlots] ints, consumed by launch_reproject_s16
+constexpr int kMinSlots = 32;
+
+
 // Device buffer that only grows (engine and WLS scratch); ensure() returns an SDR_* status.
 struct Buf {
     void* p = nullptr;
@@ -39,9 +44,11 @@ struct Geometry {
 
 // ---- prefilter / cost volume (sdr_cost.hip) ----
 struct Planes {
-    uint32_t* L;        // [F][H][W][3] 16-bit halves: {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
-    uint64_t* R;        // [F][3][H][W] int16 pairs (q(x) | q(x-1) << 16): {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
+    // per channel c of the input (cn = 1 gray, 3 colour) one operand set:
+    uint32_t* L;        // [F][H][W][3cn] 16-bit halves: {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
+    uint64_t* R;        // [F][3cn][H][W] int16 pairs (q(x) | q(x-1) << 16): {sob,sob_lo} {sob_hi,raw} {raw_lo,raw_hi}
     size_t fstrideL, fstrideR;  // elements per frame
+    int cn;
 };
 
 struct CostArgs {
@@ -111,6 +118,7 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
                       int H, int F, int ftzero, const Planes& pl, hipStream_t st);
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
+void launch_cost_cn3(const Geometry& g, const CostArgs& a, int F, hipStream_t st);  // pl.cn == 3
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
 // src may equal dst; out_min (nullable) receives min over each output frame.  median_of

@@ -518,6 +518,7 @@ static void launch_south_np(const Geometry& g, const PathLaunch& pl, const South
     dim3 block(64 * (1 + kSouthConsumers));
     switch (a.npaths) {
     case 3: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 2>), grid, block, 0, st, g, pl, a); break;
+    case 4: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 3>), grid, block, 0, st, g, pl, a); break;
     case 5: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 4>), grid, block, 0, st, g, pl, a); break;
     default: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 7>), grid, block, 0, st, g, pl, a); break;
     }

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ i
     const int tx0 = blockIdx.x * kCT, ty0 = blockIdx.y * kCT;
     const size_t fo = (size_t)blockIdx.z * W * H;
     const int t = threadIdx.x, lane = t & 63, lx = t & (kCT - 1);
-    if (out_min && t == 0 && blockIdx.x == 0 && blockIdx.y == 0) out_min[blockIdx.z] = 32767;
+    if (out_min && t < kMinSlots && blockIdx.x == 0 && blockIdx.y == 0) out_min[blockIdx.z * kMinSlots + t] = 32767;
     const int gx = tx0 + lx;
     int val[4];
 #pragma unroll
@@ -263,24 +263,47 @@ __global__ __launch_bounds__(256) void k_ccl_finalize(int* P, int* S, int n) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_ccl_apply(const int16_t* src, int16_t* dst, const int* P,
-                                                   const int* S, int n, int newVal, int maxSize,
-                                                   int* out_min) {
+// A thread owns kApplyU pixels (a grid stride apart) and walks them in phases -- all pixel and
+// label loads, then all tile-root -> global-root gathers, then all size gathers -- so its three
+// dependent memory round trips are paid once, not once per pixel.  (src and dst may be one
+// buffer: every pixel is read and then written by its own thread only.)
+constexpr int kApplyU = 2;
+__global__ __launch_bounds__(256) void k_ccl_apply(const int16_t* src, int16_t* dst,
+                                                   const int* __restrict__ P, const int* __restrict__ S,
+                                                   int n, int newVal, int maxSize, int* out_min) {
     __shared__ int wm[4];
     const size_t fo = (size_t)blockIdx.y * n;
+    const int* Pf = P + fo;
+    const int* Sf = S + fo;
+    const int stride = gridDim.x * blockDim.x;
     int m = 32767;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        int v = src[fo + i];
-        const int l = P[fo + i];
-        if (l >= 0 && S[fo + P[fo + l]] <= maxSize) v = newVal;
-        dst[fo + i] = (int16_t)v;
-        m = min(m, v);
+    for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += kApplyU * stride) {
+        int v[kApplyU], l[kApplyU], s[kApplyU];
+#pragma unroll
+        for (int u = 0; u < kApplyU; u++) {
+            const int i = min(i0 + u * stride, n - 1);  // surplus pixels repeat the last one
+            v[u] = src[fo + i];
+            l[u] = Pf[i];
+        }
+#pragma unroll
+        for (int u = 0; u < kApplyU; u++) l[u] = l[u] >= 0 ? Pf[l[u]] : -1;
+#pragma unroll
+        for (int u = 0; u < kApplyU; u++) s[u] = l[u] >= 0 ? Sf[l[u]] : 0x7fffffff;
+#pragma unroll
+        for (int u = 0; u < kApplyU; u++) {
+            const int i = i0 + u * stride;
+            if (i >= n) break;
+            const int o = s[u] <= maxSize ? newVal : v[u];
+            dst[fo + i] = (int16_t)o;
+            m = min(m, o);
+        }
     }
     if (!out_min) return;
     m = (int)wave_min_u32((uint32_t)(m + 32768)) - 32768;
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) atomicMin(&out_min[blockIdx.y], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
+    if (threadIdx.x == 0)
+        atomicMin(&out_min[blockIdx.y * kMinSlots + blockIdx.x % kMinSlots], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
 }
 
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
@@ -303,12 +326,16 @@ void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int n
     // for the label gathers), never fewer than 256 per frame
     const unsigned gb = (unsigned)min((n + 511) / 512, max(256, 2048 / F));
     hipLaunchKernelGGL(k_ccl_finalize, dim3(gb, F), dim3(256), 0, st, labels, sizes, n);
-    hipLaunchKernelGGL(k_ccl_apply, dim3(gb, F), dim3(256), 0, st, src, dst, labels, sizes, n, newVal,
+    const unsigned ga = (unsigned)min((n + 256 * kApplyU - 1) / (256 * kApplyU), max(256, 2048 / F));
+    hipLaunchKernelGGL(k_ccl_apply, dim3(ga, F), dim3(256), 0, st, src, dst, labels, sizes, n, newVal,
                        maxSize, out_min);
 }
 
 // ------------------------------------------------------------------------------------------
-// per-frame minimum (reprojectImageTo3D handleMissingValues needs min(disp))
+// per-frame minimum (reprojectImageTo3D handleMissingValues needs min(disp)), kept as kMinSlots
+// partial minima per frame: block b folds into slot b % kMinSlots and the reprojection takes the
+// minimum of the slots.  (One slot per frame serialised ~1800 same-address device-scope atomics
+// at the end of k_ccl_apply.)
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_min_s16(const int16_t* img, size_t n, size_t fstride, int* out) {
     __shared__ int wm[4];
@@ -320,7 +347,8 @@ __global__ __launch_bounds__(256) void k_min_s16(const int16_t* img, size_t n, s
     m = (int)wave_min_u32((uint32_t)(m + 32768)) - 32768;
     if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) atomicMin(&out[blockIdx.y], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
+    if (threadIdx.x == 0)
+        atomicMin(&out[blockIdx.y * kMinSlots + blockIdx.x % kMinSlots], min(min(wm[0], wm[1]), min(wm[2], wm[3])));
 }
 
 __global__ void k_init_i32(int* p, int v, int n) {
@@ -330,7 +358,8 @@ __global__ void k_init_i32(int* p, int v, int n) {
 
 void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
                     hipStream_t st) {
-    hipLaunchKernelGGL(k_init_i32, dim3((F + 255) / 256), dim3(256), 0, st, out_min, 32767, F);
+    hipLaunchKernelGGL(k_init_i32, dim3((F * kMinSlots + 255) / 256), dim3(256), 0, st, out_min, 32767,
+                       F * kMinSlots);
     dim3 grid((unsigned)min((n_per_frame + 1023) / 1024, (size_t)128), F);
     hipLaunchKernelGGL(k_min_s16, grid, dim3(256), 0, st, img, n_per_frame, fstride, out_min);
 }
@@ -375,7 +404,13 @@ __global__ __launch_bounds__(256) void k_reproject_s16(const int16_t* disp, int 
     if (x >= W) return;
     const int v = disp[(size_t)f * dfstride + (size_t)y * dstride + x];
     const double d = (double)((float)v * 0.0625f);
-    const double mind = hm ? (double)((float)mins[f] * 0.0625f) : (double)FLT_MAX;
+    double mind = (double)FLT_MAX;
+    if (hm) {
+        int m = mins[f * kMinSlots];  // wave-uniform: scalar loads
+#pragma unroll
+        for (int k = 1; k < kMinSlots; k++) m = min(m, mins[f * kMinSlots + k]);
+        mind = (double)((float)m * 0.0625f);
+    }
     reproject_px(Q, x, y, d, mind, hm, xyz + (size_t)f * xfstride + (size_t)y * xstride + 3 * (size_t)x);
 }
 

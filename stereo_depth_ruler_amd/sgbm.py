@@ -118,10 +118,12 @@ class StereoSGBM:
 
     # ---- compute ----
     def compute(self, left, right, disp=None):
-        """StereoSGBM::compute: 8-bit single-channel pair -> int16 disparity (1/16 px).
+        """StereoSGBM::compute: 8-bit pair (CV_8UC1, or CV_8UC3 whose channels' costs are summed)
+        -> int16 disparity (1/16 px).
 
-        numpy (H, W) -> numpy; torch CUDA uint8 (H, W) or (F, H, W) -> torch int16 on the same
-        device, enqueued on the current stream.
+        numpy (H, W) or (H, W, 3) -> numpy; torch CUDA uint8 (H, W), (F, H, W), (H, W, 3) or
+        (F, H, W, 3) -> torch int16 on the same device, enqueued on the current stream (a 3-dim
+        tensor whose last dimension is 3 is one colour frame).
         """
         if _is_cuda(left) or _is_cuda(right):
             return self._compute_device(left, right, disp)
@@ -133,15 +135,16 @@ class StereoSGBM:
             raise SDRError(-5, "images must be 8-bit")
         if left.ndim == 3 and left.shape[2] == 1:
             left, right = left[..., 0], right[..., 0]
-        if left.ndim != 2:
-            raise SDRError(-5, "only single-channel images are supported")
+        if not (left.ndim == 2 or (left.ndim == 3 and left.shape[2] == 3)):
+            raise SDRError(-5, "images must have 1 or 3 channels")
         left = np.ascontiguousarray(left)
         right = np.ascontiguousarray(right)
-        h, w = left.shape
+        h, w = left.shape[:2]
+        cn = 1 if left.ndim == 2 else 3
         out = disp if disp is not None else np.empty((h, w), np.int16)
         if out.shape != (h, w) or out.dtype != np.int16 or not out.flags.c_contiguous:
             raise SDRError(-1, "disp must be a C-contiguous int16 (H, W) array")
-        check(lib().sdr_sgbm_compute(self._h, left.ctypes.data, right.ctypes.data, w, h, 1, w,
+        check(lib().sdr_sgbm_compute(self._h, left.ctypes.data, right.ctypes.data, w, h, cn, w * cn,
                                      out.ctypes.data, w))
         return out
 
@@ -161,6 +164,8 @@ class StereoSGBM:
         return left.contiguous(), right.contiguous()
 
     def _compute_device(self, left, right, disp=None):
+        if left.dim() == 4 or (left.dim() == 3 and left.shape[-1] == 3):
+            return self._compute_device_color(left, right, disp)
         squeeze = left.dim() == 2
         left, right = self._prep_device(left, right)
         f, h, w = left.shape
@@ -170,6 +175,26 @@ class StereoSGBM:
         check(lib().sdr_sgbm_set_stream(self._h, _cstream(self._device)))
         check(lib().sdr_sgbm_compute_device(self._h, left.data_ptr(), right.data_ptr(), w, h, w,
                                             w * h, f, out.data_ptr(), w, w * h))
+        return out[0] if squeeze and disp is None else out
+
+    def _compute_device_color(self, left, right, disp=None):
+        if not (_is_cuda(left) and _is_cuda(right)) or left.shape != right.shape or left.dtype != right.dtype:
+            raise SDRError(-1, "left and right must be CUDA tensors of the same size and type")
+        if left.dtype != torch.uint8 or left.shape[-1] != 3:
+            raise SDRError(-5, "expected 8-bit (H, W, 3) or (F, H, W, 3) tensors")
+        if left.device.index != self._device:
+            raise SDRError(-1, f"tensors are on cuda:{left.device.index}, matcher on cuda:{self._device}")
+        squeeze = left.dim() == 3
+        if squeeze:
+            left, right = left.unsqueeze(0), right.unsqueeze(0)
+        left, right = left.contiguous(), right.contiguous()
+        f, h, w, _ = left.shape
+        out = disp if disp is not None else torch.empty((f, h, w), dtype=torch.int16, device=left.device)
+        if out.numel() != f * h * w or out.dtype != torch.int16 or not out.is_contiguous():
+            raise SDRError(-1, "disp must be a contiguous int16 tensor of the input's (F, H, W)")
+        check(lib().sdr_sgbm_set_stream(self._h, _cstream(self._device)))
+        check(lib().sdr_sgbm_compute_device_cn(self._h, left.data_ptr(), right.data_ptr(), w, h, 3, w * 3,
+                                               w * h * 3, f, out.data_ptr(), w, w * h))
         return out[0] if squeeze and disp is None else out
 
     def compute_reproject(self, left, right, Q, handleMissingValues=False, disp=None, xyz=None):

@@ -17,6 +17,16 @@ def prefilter_channels(img, ftzero):
     return sob, raw
 
 
+def cost_channels(img, ftzero):
+    """calcPixelCostBT's channels with their cost shifts: gray -> (sobel, 0), (raw, 2); an
+    interleaved 3-channel image -> the three sobels (shift 0), then the three raws (shift 2)."""
+    if img.ndim == 2:
+        s, r = prefilter_channels(img, ftzero)
+        return [(s, 0), (r, 2)]
+    per = [prefilter_channels(img[:, :, c], ftzero) for c in range(img.shape[2])]
+    return [(s, 0) for s, _ in per] + [(r, 2) for _, r in per]
+
+
 def envelope(ch):
     """(lo, hi) over the value and its two half-sample neighbours (truncating average)."""
     W = ch.shape[1]
@@ -28,19 +38,13 @@ def envelope(ch):
 
 
 def bt_cost_volume_rows(L, R, minD, D, ftzero):
-    """Pixel cost [H][W1][D] = BT(sobel) + (BT(raw) >> 2)."""
-    H, W = L.shape
+    """Pixel cost [H][W1][D] = sum over channels of BT(sobel) + (BT(raw) >> 2)."""
+    H, W = L.shape[:2]
     maxD = minD + D
     minX1, maxX1 = max(maxD, 0), W + min(minD, 0)
     out = np.zeros((H, maxX1 - minX1, D), np.int32)
-    chans = []
-    for img in (L, R):
-        s, r = prefilter_channels(img, ftzero)
-        chans.append((s, r))
     xs = np.arange(minX1, maxX1)
-    for c, scale in ((0, 0), (1, 2)):
-        u = chans[0][c]
-        v = chans[1][c]
+    for (u, scale), (v, _) in zip(cost_channels(L, ftzero), cost_channels(R, ftzero)):
         u0, u1 = envelope(u)
         v0, v1 = envelope(v)
         for di, d in enumerate(range(minD, maxD)):
@@ -82,7 +86,7 @@ def cost_volume(L, R, minD, D, bs, P2, ftzero, hh=False):
 # whole rows.  The oracle instead follows OpenCV's row drivers (ring buffers, running sums, packed
 # per-pixel loops).  Agreement between the two pins the oracle's transcription of A.4-A.9.
 
-SGM_SGBM, SGM_HH, SGM_3WAY = 0, 1, 2
+SGM_SGBM, SGM_HH, SGM_3WAY, SGM_HH4 = 0, 1, 2, 3
 _BIG = 1 << 40  # the d = -1 / d = D neighbours: never the minimum
 
 # predecessor offsets: the predecessor of (x, y) along r is (x - dx, y - dy)
@@ -90,6 +94,7 @@ SGM_DIRS = {
     SGM_SGBM: [(1, 0), (1, 1), (0, 1), (-1, 1), (-1, 0)],
     SGM_HH: [(1, 0), (1, 1), (0, 1), (-1, 1), (-1, 0), (-1, -1), (0, -1), (1, -1)],
     SGM_3WAY: [(1, 0), (-1, 0), (0, 1)],
+    SGM_HH4: [(1, 0), (-1, 0), (0, 1), (0, -1)],
 }
 
 
@@ -226,7 +231,7 @@ def sgm_full_volume(L, R, minD, D, bs, P1, P2, d12, cap, uniq, ws=0, sr=0, mode=
                     nstripes=4, uniq_rule=0, stages=3):
     """StereoSGBM::compute as a materialised-volume formulation.  stages: 1 median, 2 speckle."""
     e = sgm_effective(minD, D, bs, P1, P2, d12, cap, uniq, mode, uniq_rule)
-    H, W = L.shape
+    H, W = L.shape[:2]
     minX1, maxX1 = max(e["maxD"], 0), W + min(minD, 0)
     W1 = maxX1 - minX1
     inv = (minD - 1) * 16
@@ -248,7 +253,7 @@ def sgm_full_volume(L, R, minD, D, bs, P1, P2, d12, cap, uniq, ws=0, sr=0, mode=
         segs = [(0, H, 0)]
     raw = np.full((H, W), inv, np.int64)
     for s0, end, out0 in segs:
-        C = e["P2"] + _box_rows(hs, s0, end, e["SH2"], mode == SGM_HH)
+        C = e["P2"] + _box_rows(hs, s0, end, e["SH2"], mode in (SGM_HH, SGM_HH4))
         assert C.max() <= 32767, "outside the int16 cost domain"
         Ssum = np.zeros_like(C)
         for dx, dy in SGM_DIRS[mode]:

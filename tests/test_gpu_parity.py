@@ -63,6 +63,9 @@ CASES = [
     (40, 200, 64, 0, 11, 0, 12, (30, 2), 1, 600, 2400, 63, 18),         # largest block (11x11)
     (44, 210, 48, 2, 11, 0, 10, (0, 0), 1, 600, 2400, 63, 19),          # 3WAY, 11x11
     (36, 300, 256, 0, 9, 0, 12, (0, 0), 1, 600, 2400, 63, 20),          # D = 256, 5-path
+    (33, 100, 16, 3, 5, 0, 12, (20, 2), 1, 600, 2400, 63, 21),          # MODE_HH4 (4 paths)
+    (48, 200, 128, 3, 3, -6, 10, (0, 0), 1, 300, 1800, 31, 22),         # MODE_HH4, minD < 0
+    (40, 320, 208, 3, 7, 0, 5, (50, 2), 2, 100, 900, 15, 23),           # MODE_HH4, D > 128
 ]
 
 
@@ -97,7 +100,7 @@ def test_uniqueness_rule_switch(oracle, rule, mode):
 
 def test_cost_volume_bit_exact(oracle):
     L, R, _ = S.make_pair(40, 150, 48, seed=23)
-    for mode in (0, 1):
+    for mode in (0, 1, 3):
         args = (0, 48, 5, 600, 2400, 1, 63, 12, 0, 0, mode)
         m = sdr.StereoSGBM.create(*args)
         m.compute(L, R)
@@ -265,7 +268,7 @@ def test_errors_mirror_opencv_asserts():
         sdr.StereoSGBM.create(0, 100, 5).compute(L, L)
     assert e.value.code == -2
     with pytest.raises(sdr.SDRError) as e:
-        sdr.StereoSGBM.create(0, 16, 5, mode=3).compute(L, L)
+        sdr.StereoSGBM.create(0, 16, 5, mode=7).compute(L, L)
     assert e.value.code == -3
     with pytest.raises(sdr.SDRError):
         sdr.StereoSGBM.create(0, 16, 5).compute(L, np.zeros((20, 65), np.uint8))

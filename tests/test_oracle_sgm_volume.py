@@ -84,3 +84,71 @@ def test_int16_domain_bound_is_tight():
             p2 = p2_domain_max(bs, cap, 0)
             cmax = p2 + (2 * ft + 63) * bs * bs
             assert cmax + p2 <= 32767 < cmax + p2 + 2
+
+
+def color_pair(H, W, D, seed):
+    """3-channel pair whose channels differ: a seeded gray pair, one channel shifted in
+    intensity, one replaced by noise (so every channel's Sobel and raw costs matter)."""
+    L, R = S.adversarial_pair("noise" if seed % 2 else "binary", H, W, D, seed=seed)
+    rng = np.random.default_rng(seed)
+    Lc = np.stack([L, np.clip(L.astype(int) + 40, 0, 255), rng.integers(0, 256, L.shape)], -1)
+    Rc = np.stack([R, np.clip(R.astype(int) + 40, 0, 255), rng.integers(0, 256, R.shape)], -1)
+    return Lc.astype(np.uint8), Rc.astype(np.uint8)
+
+
+@pytest.mark.parametrize("mode,bs,minD,D,cap", [(0, 5, 0, 32, 63), (1, 3, -5, 16, 31), (2, 7, 3, 48, 15)])
+def test_color_cost_volume_vs_numpy(oracle, mode, bs, minD, D, cap):
+    """calcPixelCostBT's cn == 3 branch: per-channel Sobel and raw costs summed."""
+    L, R = color_pair(13, D + max(minD, 0) + 40, D, seed=bs)
+    p = oracle.make_params(minD, D, bs, 8, 96, 1, cap, 0, 0, 0, mode)
+    e = N.sgm_effective(minD, D, bs, 8, 96, 1, cap, 0, mode)
+    got = oracle.cost_volume(L, R, p)
+    ref = N.cost_volume(L, R, minD, D, 2 * e["SW2"] + 1, e["P2"], e["ftzero"], hh=(mode == 1))
+    assert np.array_equal(got, ref)
+    # a colour pair with equal channels costs exactly 3x the gray pair's pixel cost
+    g = L[:, :, 0]
+    Lg = np.repeat(g[:, :, None], 3, -1)
+    Rg = np.repeat(R[:, :, 0][:, :, None], 3, -1)
+    pg = N.bt_cost_volume_rows(g, R[:, :, 0], minD, D, e["ftzero"])
+    assert np.array_equal(N.bt_cost_volume_rows(Lg, Rg, minD, D, e["ftzero"]), 3 * pg)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_color_oracle_matches_volume_formulation(oracle, seed):
+    rng = np.random.default_rng(500 + seed)
+    mode = seed % 3
+    D = int(rng.choice([16, 32]))
+    bs = int(rng.choice([1, 3, 5]))
+    minD = int(rng.integers(-8, 4))
+    cap = int(rng.choice([15, 31]))
+    P1 = int(rng.integers(1, 100))
+    P2 = int(rng.integers(P1 + 1, 1000))
+    args = (minD, D, bs, P1, P2, 1, cap, int(rng.choice([0, 10])), 20 * (seed % 2), 1, mode)
+    L, R = color_pair(int(rng.integers(8, 24)), D + max(minD, 0) + int(rng.integers(10, 60)), D, seed)
+    for stages in (0, 3):
+        ref = oracle.sgbm_compute(L, R, oracle.make_params(*args), stages=stages)
+        got = N.sgm_full_volume(L, R, *args, stages=stages)
+        assert np.array_equal(ref, got), f"stages={stages}: {(ref != got).sum()} px differ"
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_hh4_oracle_matches_volume_formulation(oracle, seed):
+    """MODE_HH4 (computeDisparitySGBM_HH4: vertical sums over a full-DP cost buffer, then the two
+    horizontal directions with the WTA): 4 paths, MODE_HH's cost rows, the scalar uniqueness rule."""
+    case = random_case(100 + seed)
+    a = list(case["args"])
+    a[10] = 3  # MODE_HH4
+    a[4] = min(a[4], p2_domain_max(a[2], a[6], 1))
+    L, R = S.adversarial_pair(case["kind"], case["H"], case["W"], a[1], seed=case["seed"])
+    for stages in (0, 3):
+        ref = oracle.sgbm_compute(L, R, oracle.make_params(*a), stages=stages)
+        got = N.sgm_full_volume(L, R, *a, stages=stages)
+        assert np.array_equal(ref, got), f"stages={stages}: {(ref != got).sum()} px differ"
+
+
+def test_hh4_differs_from_hh(oracle):
+    L, R = S.adversarial_pair("textured", 30, 120, 32, seed=4)
+    args = [0, 32, 5, 60, 600, 1, 63, 10, 0, 0, 3]
+    hh4 = oracle.sgbm_compute(L, R, oracle.make_params(*args))
+    args[10] = 1
+    assert (hh4 != oracle.sgbm_compute(L, R, oracle.make_params(*args))).sum() > 0

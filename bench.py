@@ -180,7 +180,11 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=8, help="distinct resident frames per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the per-kernel HIP-event segment after the timed region (no roofline)")
+    ap.add_argument("--in-flight-timing", action="store_true",
+                    help="also put HIP events around matcher 0's launches inside the timed region "
+                         "(roofline.in_flight; the events cost ~2 %% of the frame rate)")
     ap.add_argument("--streams", type=int, default=3, help="frames in flight (one matcher + stream each)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -299,7 +303,7 @@ def main():
             p.wait()
     pending = [None] * (2 * ns)
     torch.cuda.synchronize()
-    if not a.no_kernel_timing:
+    if not a.no_kernel_timing and a.in_flight_timing:
         m.enable_timing(2)
         m.kernel_time(-1, reset=True)
     if world > 1:
@@ -386,28 +390,32 @@ def main():
     roofline = None
     kernels = None
     if not a.no_kernel_timing:
-        kernels, inflight = kernel_report(m)
-        roofline = inflight
-        if inflight is not None:
-            inflight["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
-                                    f"({ns} frames in flight: an event pair also spans the wait for CUs "
-                                    f"held by the other streams' kernels, so it overstates the duration)")
-        if ns > 1 and inflight is not None:
-            # the dominant kernel's roofline: the same launches with nothing beside them, a
-            # single-stream segment timed right after the timed region (rocprofv3's per-dispatch
-            # durations of these launches agree: profiles/r1_segments_c2.md)
-            torch.cuda.synchronize()
-            m.kernel_time(-1, reset=True)
-            with torch.cuda.stream(streams[0]):
-                for i in range(a.iso_steps):
-                    j = (i * batch) % (nf - batch + 1) if nf > batch else 0
-                    run(j, 0, 0)
-            torch.cuda.synchronize()
-            iso_k, roofline = kernel_report(m)
+        inflight = None
+        if a.in_flight_timing:
+            _, inflight = kernel_report(m)
+            if inflight is not None:
+                inflight["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
+                                        f"({ns} frames in flight: an event pair also spans the wait for CUs "
+                                        f"held by the other streams' kernels, so it overstates the duration)")
+        # the dominant kernel's roofline: the same launches with nothing beside them, a
+        # single-stream segment timed right after the timed region (no events inside the timed
+        # region; rocprofv3's per-dispatch durations of these launches agree:
+        # profiles/r2_segments_c2.md)
+        torch.cuda.synchronize()
+        m.enable_timing(2)
+        m.kernel_time(-1, reset=True)
+        with torch.cuda.stream(streams[0]):
+            for i in range(a.iso_steps):
+                j = (i * batch) % (nf - batch + 1) if nf > batch else 0
+                run(j, 0, 0)
+        torch.cuda.synchronize()
+        kernels, roofline = kernel_report(m)
+        if roofline is not None:
             roofline["measured"] = (f"HIP events around each launch, {a.iso_steps} single-stream steps "
                                     f"after the timed region")
-            roofline["kernels"] = iso_k
-            roofline["in_flight"] = inflight
+            roofline["kernels"] = kernels
+            if inflight is not None:
+                roofline["in_flight"] = inflight
         m.enable_timing(0)
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6

@@ -249,15 +249,21 @@ __global__ __launch_bounds__(256) void k_ccl_merge(const int16_t* __restrict__ i
     }
 }
 
-// tile roots (S > 0): global root, size accumulated there, one-hop pointer for apply
-__global__ __launch_bounds__(256) void k_ccl_finalize(int* P, int* S, int n) {
+// tile roots (S > 0): global root, size accumulated there, one-hop pointer for apply.  Only
+// "size <= maxSize" is ever asked, so a tile part larger than maxSize marks its component with a
+// plain store of kBigComponent instead of adding (every atomic add to a large component's root
+// serialises at that one address; the store may land before or after the adds of other parts,
+// and either way the size reads as more than maxSize).
+constexpr int kBigComponent = 0x40000000;
+__global__ __launch_bounds__(256) void k_ccl_finalize(int* P, int* S, int n, int maxSize) {
     const size_t fo = (size_t)blockIdx.y * n;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int c = S[fo + i];
         if (c <= 0) continue;
         const int g = uf_find(P + fo, i);
         if (g != i) {
-            atomicAdd(&S[fo + g], c);
+            if (c > maxSize) S[fo + g] = kBigComponent;
+            else atomicAdd(&S[fo + g], c);
             P[fo + i] = g;
         }
     }
@@ -325,7 +331,7 @@ void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int n
     // frame: 44 -> 34 us for the four speckle kernels; 256 blocks per frame left one wave per SIMD
     // for the label gathers), never fewer than 256 per frame
     const unsigned gb = (unsigned)min((n + 511) / 512, max(256, 2048 / F));
-    hipLaunchKernelGGL(k_ccl_finalize, dim3(gb, F), dim3(256), 0, st, labels, sizes, n);
+    hipLaunchKernelGGL(k_ccl_finalize, dim3(gb, F), dim3(256), 0, st, labels, sizes, n, maxSize);
     const unsigned ga = (unsigned)min((n + 256 * kApplyU - 1) / (256 * kApplyU), max(256, 2048 / F));
     hipLaunchKernelGGL(k_ccl_apply, dim3(ga, F), dim3(256), 0, st, src, dst, labels, sizes, n, newVal,
                        maxSize, out_min);

@@ -405,13 +405,13 @@ def main():
         m.enable_timing(2)
         m.kernel_time(-1, reset=True)
         with torch.cuda.stream(streams[0]):
-            for i in range(a.iso_steps):
+            for i in range(max(1, a.iso_steps)):
                 j = (i * batch) % (nf - batch + 1) if nf > batch else 0
                 run(j, 0, 0)
         torch.cuda.synchronize()
         kernels, roofline = kernel_report(m)
         if roofline is not None:
-            roofline["measured"] = (f"HIP events around each launch, {a.iso_steps} single-stream steps "
+            roofline["measured"] = (f"HIP events around each launch, {max(1, a.iso_steps)} single-stream steps "
                                     f"after the timed region")
             roofline["kernels"] = kernels
             if inflight is not None:

@@ -153,20 +153,21 @@ __device__ __forceinline__ Rsrc rsrc_at(const void* base) {
 
 // K packed pairs at the lane's byte offset vofs plus a wave-uniform (SGPR) byte offset sofs: one
 // resource per buffer for a whole chain, and one scalar add per step moves every access of the step
-template <int K>
+// (AUX: the cache-policy bits; 2 = non-temporal)
+template <int K, int AUX = 0>
 __device__ __forceinline__ Regs<K> load_buf(Rsrc r, uint32_t vofs, uint32_t sofs = 0) {
     Regs<K> v;
     if constexpr (K == 1) {
-        v.r[0] = __builtin_amdgcn_raw_buffer_load_b32(r, vofs, sofs, 0);
+        v.r[0] = __builtin_amdgcn_raw_buffer_load_b32(r, vofs, sofs, AUX);
     } else if constexpr (K == 2) {
-        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, vofs, sofs, 0);
+        const auto t = __builtin_amdgcn_raw_buffer_load_b64(r, vofs, sofs, AUX);
         v.r[0] = t[0];
         v.r[1] = t[1];
     } else {
         static_assert(K % 4 == 0, "K = 1, 2 or a multiple of 4");
 #pragma unroll
         for (int j = 0; j < K / 4; j++) {
-            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, vofs + 16 * j, sofs, 0);
+            const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, vofs + 16 * j, sofs, AUX);
             v.r[4 * j] = t[0]; v.r[4 * j + 1] = t[1]; v.r[4 * j + 2] = t[2]; v.r[4 * j + 3] = t[3];
         }
     }

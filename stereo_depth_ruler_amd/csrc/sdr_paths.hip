@@ -97,6 +97,13 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
 }
 
 constexpr int kPathsLA = 16;  // k_paths lookahead (steps)
+// k_paths loads C with the default cache policy: the launch's four directions (and k_south_wta
+// after it) re-read C, and the 212 MB volume of a C2 frame is served partly from the 256 MB
+// Infinity Cache -- non-temporal C loads there measured 274 -> 340 us.
+// k_south_wta is the last reader of both C and the L records, and loads them non-temporal: the
+// consumers' L records (849 MB a C2 frame) then stop evicting C and each other from the caches,
+// 219 -> 183 us (MI355X, scripts/kbench.py A/B, bit-exact).
+constexpr int kLoadNT = 2;
 
 template <int DPL, bool PAD>
 __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             auto st = [&](const int, auto jc) __attribute__((always_inline)) {
                 constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
                 const Regs<K> c = cring[j];
-                cring[(j + LA) % R] = load_buf<K>(rsrc_at(cp), lofs);
+                cring[(j + LA) % R] = load_buf<K, kLoadNT>(rsrc_at(cp), lofs);
                 cp += rowb;
                 const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
 #pragma unroll
@@ -331,7 +338,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     }
     const char* lbase = (const char*)(a.L + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
     auto oload = [&](int q, int blk, int ps) __attribute__((always_inline)) {
-        return load_buf<WK>(rsrc_at(lbase + (ptrdiff_t)blk * bstepb), lofs[ps] + (uint32_t)(q * D * 2));
+        return load_buf<WK, kLoadNT>(rsrc_at(lbase + (ptrdiff_t)blk * bstepb), lofs[ps] + (uint32_t)(q * D * 2));
     };
     // rows before kw belong to the previous 3WAY stripe: recurred through, never output
     const int kw = ch.kwrite;

@@ -174,21 +174,23 @@ __device__ __forceinline__ Regs<K> load_buf(Rsrc r, uint32_t vofs, uint32_t sofs
     return v;
 }
 
-// non-temporal (aux = nt) stores of K packed pairs
-template <int K>
+// non-temporal (aux = nt) stores of K packed pairs (k_paths' L records: default-policy stores
+// measured 274 -> 300 us there and made k_south_wta's reads 181 -> 200 us; sc0/sc1 variants of
+// the loads and stores measured the same as nt within noise)
+template <int K, int AUX = 2>
 __device__ __forceinline__ void store_buf_nt(Rsrc r, uint32_t vofs, uint32_t sofs, const Regs<K>& v) {
     if constexpr (K == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(v.r[0], r, vofs, sofs, 2);
+        __builtin_amdgcn_raw_buffer_store_b32(v.r[0], r, vofs, sofs, AUX);
     } else if constexpr (K == 2) {
         __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) uint32_t){v.r[0], v.r[1]}, r,
-                                              vofs, sofs, 2);
+                                              vofs, sofs, AUX);
     } else {
 #pragma unroll
         for (int j = 0; j < K / 4; j++)
             __builtin_amdgcn_raw_buffer_store_b128(
                 (__attribute__((ext_vector_type(4))) uint32_t){v.r[4 * j], v.r[4 * j + 1], v.r[4 * j + 2],
                                                                v.r[4 * j + 3]},
-                r, vofs + 16 * j, sofs, 2);
+                r, vofs + 16 * j, sofs, AUX);
     }
 }
 

@@ -35,7 +35,8 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-HOST_ASAN = ["-g", "-fno-omit-frame-pointer"] + [x for f in ("-fsanitize=address", "-fsanitize=undefined",
+# host-only debug info: device debug info of the unrolled cost kernels takes hipcc tens of minutes
+HOST_ASAN = ["-Xarch_host", "-g", "-fno-omit-frame-pointer"] + [x for f in ("-fsanitize=address", "-fsanitize=undefined",
                                                             "-fno-sanitize-recover=undefined")
                                                  for x in ("-Xarch_host", f)]
 

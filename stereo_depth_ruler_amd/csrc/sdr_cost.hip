@@ -1,9 +1,10 @@
 // sdr_cost.hip -- A.1 prefilter + BT operands and A.2/A.3 cost volume kernels (CDNA4).
 //
-//   L pack    u32 [F][H][W][3]  the left image's BT operands at x as 16-bit halves:
-//                               {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
-//   planes R  u64 [F][3][H][W]  int16 PAIRS of the right image's operands: q(x) | q(x-1) << 16, so a
-//                               lane holding disparities (d, d+1) reads one word for xr = x-d, x-d-1
+//   L pack    u32 [F][H][W][3cn]  the left image's BT operands at x as 16-bit halves, per channel:
+//                                 {sob | sob_lo<<16} {sob_hi | raw<<16} {raw_lo | raw_hi<<16}
+//   planes R  u64 [F][3cn][H][W]  int16 PAIRS of the right image's operands: q(x) | q(x-1) << 16, so
+//                                 a lane holding disparities (d, d+1) reads one word for xr = x-d, x-d-1
+//   (cn = 1 for gray input, 3 for CV_8UC3: calcPixelCostBT sums the channels' costs)
 //   C         s16 [F][H][W1][D] P2 + blockSize^2 box sum of the BT pixel cost
 //
 // Cost kernel: lanes = disparity pairs (as in the path kernels).  A block owns BCOLS output
@@ -11,8 +12,9 @@
 // computed once (the four waves own interleaved columns), summed vertically in registers (a ring
 // of the last NR rows, static slots by unrolling the row loop by the window height), and the
 // column sums are exchanged through LDS for the horizontal sums.  A pixel's left operands are
-// the same for all lanes: they are read from LDS as broadcasts and reach the packed ops through
-// op_sel half selection.  The right image's pair planes are staged per row (split into even/odd-x
+// the same for all lanes: they are read from LDS as 16-byte broadcasts (one per column and
+// channel) and reach the packed ops through op_sel half selection.  The kernel template itself is
+// in sdr_cost_kernel.hpp (gray instantiations here, colour ones in sdr_cost3.hip).  The right image's pair planes are staged per row (split into even/odd-x
 // halves so that lane p reading entry x - 2p is bank-conflict free), fetched two rows ahead
 // through registers and double-buffered in LDS.  One barrier per row.
 #include "sdr_device.hpp"

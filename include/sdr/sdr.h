@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SDR_ABI_VERSION 2
+#define SDR_ABI_VERSION 3
 
 /* cv::StereoSGBM::MODE_* */
 enum { SDR_MODE_SGBM = 0, SDR_MODE_HH = 1, SDR_MODE_SGBM_3WAY = 2, SDR_MODE_HH4 = 3 };
@@ -181,7 +181,17 @@ typedef struct sdr_wls_params {
     int num_iter;                   /* FGS iterations (3) */
     int left_offset, right_offset, top_offset, bottom_offset;
     int min_disp;                   /* outside-ROI value is 16*(min_disp-1) */
+    int fgs_solver;                 /* SDR_FGS_PCR (default) or SDR_FGS_THOMAS (below) */
 } sdr_wls_params;
+
+/* Solver of the FGS line systems (I + lambda*L) u = f.  ximgproc runs the sequential Thomas
+ * elimination; SDR_FGS_THOMAS reproduces it operation for operation (bit-exact with
+ * oracle/wls_oracle.c fgs_line), one lane per image line.  SDR_FGS_PCR (default) solves the same
+ * systems by parallel cyclic reduction, a workgroup per line, with the diagonal carried as the
+ * row sum: it is ~200x closer to the exact solution than the sequential sweep in float32 and
+ * differs from it by at most 1 int16 level in the WLS output (tests/test_gpu_wls.py); lines of at
+ * most 4096 samples. */
+enum { SDR_FGS_PCR = 0, SDR_FGS_THOMAS = 1 };
 
 /* cv::ximgproc::createDisparityWLSFilter(matcher_left) (stereo_disparity.cpp:11): fills the
  * filter parameters for an SGBM left matcher AND mutates the matcher's parameters the way
@@ -209,10 +219,11 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_rig
                    const uint8_t* guide, int width, int height, size_t guide_stride,
                    int16_t* out, float* conf);
 /* cv::ximgproc::fastGlobalSmootherFilter(guide, src, dst, lambda, sigma, attenuation, iters) on
- * nimg float images [nimg][h][w] sharing one 8-bit guide, in place, async on `stream`. */
+ * nimg float images [nimg][h][w] sharing one 8-bit guide, in place, async on `stream`; solver
+ * SDR_FGS_PCR or SDR_FGS_THOMAS. */
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
                           double lambda, double sigma_color, double lambda_attenuation,
-                          int num_iter, float* d_img, int nimg, void* stream);
+                          int num_iter, float* d_img, int nimg, int solver, void* stream);
 
 /* ---- ingest in front of the path: StereoRectifier + SBS split ----
  * cv::initUndistortRectifyMap(K, dist, R, P, size, CV_16SC2, map1, map2)   stereo_rectifier.cpp:7-11

@@ -253,6 +253,9 @@ public:
     void setLRCthresh(int v) { p_.lrc_thresh = v; push(); }
     int getDepthDiscontinuityRadius() const { return p_.depth_discontinuity_radius; }
     void setDepthDiscontinuityRadius(int v) { p_.depth_discontinuity_radius = v; push(); }
+    // engine extension: FGS line solver, SDR_FGS_PCR (default) or SDR_FGS_THOMAS (sdr.h)
+    int getFgsSolver() const { return p_.fgs_solver; }
+    void setFgsSolver(int v) { p_.fgs_solver = v; push(); }
 
     // filter(disparity_map_left CV_16S, left_view CV_8UC1, filtered CV_16S, disparity_map_right CV_16S)
     void filter(const Mat& dl, const Mat& left_view, Mat& filtered, const Mat& dr) {

@@ -48,7 +48,11 @@ class WlsParams(ctypes.Structure):
                 ("lrc_thresh", ctypes.c_int), ("depth_disc_radius", ctypes.c_int),
                 ("roll_off", ctypes.c_float), ("lambda_attenuation", ctypes.c_double),
                 ("num_iter", ctypes.c_int), ("roi_x", ctypes.c_int), ("roi_y", ctypes.c_int),
-                ("roi_w", ctypes.c_int), ("roi_h", ctypes.c_int), ("min_disp", ctypes.c_int)]
+                ("roi_w", ctypes.c_int), ("roi_h", ctypes.c_int), ("min_disp", ctypes.c_int),
+                ("fgs_solver", ctypes.c_int)]
+
+
+FGS_PCR, FGS_THOMAS = 0, 1  # orc_wls_params.fgs_solver (wls_oracle.h)
 
 
 def lib():
@@ -83,6 +87,8 @@ def lib():
         L.orc_fgs_lut.argtypes = [ctypes.c_double, f32p]
         L.orc_wls_disc_map.argtypes = [i16p, ci, ci, ci, ci, ci, ci, ci, ctypes.c_float, f32p]
         L.orc_wls_confidence.argtypes = [i16p, i16p, ci, ci, wp, f32p]
+        L.orc_fgs_filter_f32_ex.argtypes = [u8p, sz, ci, ci, ctypes.c_double, ctypes.c_double,
+                                             ctypes.c_double, ci, ci, f32p]
         L.orc_fgs_filter_f32.argtypes = [u8p, sz, ci, ci, ctypes.c_double, ctypes.c_double,
                                          ctypes.c_double, ci, f32p]
         L.orc_wls_filter.argtypes = [i16p, i16p, u8p, sz, ci, ci, wp, i16p, f32p]
@@ -246,12 +252,14 @@ def wls_confidence(dl, dr, p: WlsParams):
     return out
 
 
-def fgs_filter(guide, img, lambda_, sigma_color, attenuation=0.25, num_iter=3):
+def fgs_filter(guide, img, lambda_, sigma_color, attenuation=0.25, num_iter=3, solver=FGS_PCR):
+    """FastGlobalSmootherFilter; solver FGS_PCR (the engine's default) or FGS_THOMAS (ximgproc's
+    sequential sweep)."""
     guide = np.ascontiguousarray(guide, np.uint8)
     out = np.array(img, dtype=np.float32, copy=True, order="C")
     h, w = out.shape
-    lib().orc_fgs_filter_f32(_p(guide, ctypes.c_uint8), guide.strides[0], w, h, lambda_, sigma_color,
-                             attenuation, num_iter, _p(out, ctypes.c_float))
+    lib().orc_fgs_filter_f32_ex(_p(guide, ctypes.c_uint8), guide.strides[0], w, h, lambda_, sigma_color,
+                                attenuation, num_iter, int(solver), _p(out, ctypes.c_float))
     return out
 
 

@@ -30,6 +30,7 @@ void orc_wls_params_for_sgbm(int minDisparity, int numDisparities, int blockSize
     p->roi_w = width - l - r;
     p->roi_h = height;
     p->min_disp = minDisparity;
+    p->fgs_solver = ORC_FGS_PCR;
 }
 
 void orc_fgs_lut(double sigma_color, float* lut) {
@@ -117,12 +118,61 @@ static void fgs_line(float* u, const float* C, float* t, int n, size_t s, float 
     for (int k = n - 2; k >= 0; k--) u[(size_t)k * s] = u[(size_t)k * s] - t[(size_t)k * s] * u[(size_t)(k + 1) * s];
 }
 
-void orc_fgs_filter_f32(const uint8_t* g, size_t gs, int w, int h, double lambda, double sigma,
-                        double att, int iters, float* img) {
+/* The same system solved by parallel cyclic reduction (the engine's k_fgs_pcr follows this
+ * operation order exactly).  Equation k of a line: a_k u_{k-1} + b_k u_k + c_k u_{k+1} = d_k with
+ *   c_k = lam*C[k] <= 0,  a_k = lam*C[k-1] <= 0 (0 at k = 0),  row sum e_k = a_k + b_k + c_k = 1.
+ * Stage s (s = 1, 2, 4, ... < n) eliminates u_{k-s} and u_{k+s} from every equation at once,
+ * using the neighbours' reciprocal diagonals r = 1/b (zeros stand for a missing neighbour):
+ *   k1 = a_k r_{k-s} <= 0;  k2 = c_k r_{k+s} <= 0
+ *   a_k' = -(a_{k-s} k1);  c_k' = -(c_{k+s} k2);  e_k' = (e_k - e_{k-s} k1) - e_{k+s} k2
+ *   b_k' = (e_k' - a_k') - c_k';   d_k' = (d_k - d_{k-s} k1) - d_{k+s} k2
+ * after which every equation is decoupled: u_k = d_k / b_k.  The diagonal is carried as the row
+ * sum (the system is an M-matrix: every term of e' and b' is non-negative), never as
+ * b - c k1 - a k2, whose terms cancel to about 1/(4 lam) of their size at lam = 8000 and would
+ * lose ~14 bits per stage.  `w` holds 11 floats per sample. */
+static void fgs_line_pcr(float* u, const float* C, float* w, int n, size_t s, float lam) {
+    float *a = w, *e = w + n, *c = w + 2 * n, *d = w + 3 * n, *r = w + 4 * n, *b = w + 5 * n;
+    float *a2 = w + 6 * n, *e2 = w + 7 * n, *c2 = w + 8 * n, *d2 = w + 9 * n, *b2 = w + 10 * n;
+    for (int k = 0; k < n; k++) {
+        c[k] = lam * C[(size_t)k * s];
+        a[k] = k > 0 ? lam * C[(size_t)(k - 1) * s] : 0.0f;
+        e[k] = 1.0f;
+        b[k] = (1.0f - a[k]) - c[k];
+        d[k] = u[(size_t)k * s];
+    }
+    for (int st = 1; st < n; st *= 2) {
+        for (int k = 0; k < n; k++) r[k] = 1.0f / b[k];
+        for (int k = 0; k < n; k++) {
+            const int m = k - st, q = k + st;
+            const float am = m >= 0 ? a[m] : 0.0f, em = m >= 0 ? e[m] : 0.0f;
+            const float dm = m >= 0 ? d[m] : 0.0f, rm = m >= 0 ? r[m] : 0.0f;
+            const float cp = q < n ? c[q] : 0.0f, ep = q < n ? e[q] : 0.0f;
+            const float dp = q < n ? d[q] : 0.0f, rp = q < n ? r[q] : 0.0f;
+            const float k1 = a[k] * rm;
+            const float k2 = c[k] * rp;
+            a2[k] = -(am * k1);
+            c2[k] = -(cp * k2);
+            e2[k] = (e[k] - em * k1) - ep * k2;
+            b2[k] = (e2[k] - a2[k]) - c2[k];
+            d2[k] = (d[k] - dm * k1) - dp * k2;
+        }
+        float* t;
+        t = a; a = a2; a2 = t;
+        t = e; e = e2; e2 = t;
+        t = c; c = c2; c2 = t;
+        t = d; d = d2; d2 = t;
+        t = b; b = b2; b2 = t;
+    }
+    for (int k = 0; k < n; k++) u[(size_t)k * s] = d[k] / b[k];
+}
+
+void orc_fgs_filter_f32_ex(const uint8_t* g, size_t gs, int w, int h, double lambda,
+                           double sigma, double att, int iters, int solver, float* img) {
     float* lut = (float*)malloc(sizeof(float) * FGS_LEVELS);
     float* Ch = (float*)malloc(sizeof(float) * (size_t)w * h);
     float* Cv = (float*)malloc(sizeof(float) * (size_t)w * h);
-    float* t = (float*)malloc(sizeof(float) * (size_t)w * h);
+    const int nmax = w > h ? w : h;
+    float* t = (float*)malloc(sizeof(float) * ((size_t)w * h > (size_t)11 * nmax ? (size_t)w * h : (size_t)11 * nmax));
     orc_fgs_lut(sigma, lut);
     for (int i = 0; i < h; i++)
         for (int j = 0; j < w; j++) {
@@ -134,14 +184,24 @@ void orc_fgs_filter_f32(const uint8_t* g, size_t gs, int w, int h, double lambda
         }
     float lam = (float)lambda;
     for (int n = 0; n < iters; n++) {
-        for (int i = 0; i < h; i++) fgs_line(img + (size_t)i * w, Ch + (size_t)i * w, t + (size_t)i * w, w, 1, lam);
-        for (int j = 0; j < w; j++) fgs_line(img + j, Cv + j, t + j, h, (size_t)w, lam);
+        if (solver == ORC_FGS_THOMAS) {
+            for (int i = 0; i < h; i++) fgs_line(img + (size_t)i * w, Ch + (size_t)i * w, t + (size_t)i * w, w, 1, lam);
+            for (int j = 0; j < w; j++) fgs_line(img + j, Cv + j, t + j, h, (size_t)w, lam);
+        } else {
+            for (int i = 0; i < h; i++) fgs_line_pcr(img + (size_t)i * w, Ch + (size_t)i * w, t, w, 1, lam);
+            for (int j = 0; j < w; j++) fgs_line_pcr(img + j, Cv + j, t, h, (size_t)w, lam);
+        }
         lam = lam * (float)att;
     }
     free(lut);
     free(Ch);
     free(Cv);
     free(t);
+}
+
+void orc_fgs_filter_f32(const uint8_t* g, size_t gs, int w, int h, double lambda, double sigma,
+                        double att, int iters, float* img) {
+    orc_fgs_filter_f32_ex(g, gs, w, h, lambda, sigma, att, iters, ORC_FGS_THOMAS, img);
 }
 
 /* saturate_cast<short>(float) = saturate_cast<short>(cvRound(v)): round to nearest even; cvRound
@@ -170,8 +230,10 @@ void orc_wls_filter(const int16_t* dl, const int16_t* dr, const uint8_t* guide, 
                 dc[(size_t)i * rw + j] = conf[o] * (float)dl[o];
             }
         const uint8_t* g = guide + (size_t)p->roi_y * gs + p->roi_x;
-        orc_fgs_filter_f32(g, gs, rw, rh, p->lambda, p->sigma_color, p->lambda_attenuation, p->num_iter, dc);
-        orc_fgs_filter_f32(g, gs, rw, rh, p->lambda, p->sigma_color, p->lambda_attenuation, p->num_iter, cc);
+        orc_fgs_filter_f32_ex(g, gs, rw, rh, p->lambda, p->sigma_color, p->lambda_attenuation, p->num_iter,
+                              p->fgs_solver, dc);
+        orc_fgs_filter_f32_ex(g, gs, rw, rh, p->lambda, p->sigma_color, p->lambda_attenuation, p->num_iter,
+                              p->fgs_solver, cc);
         for (int i = 0; i < rh; i++)
             for (int j = 0; j < rw; j++) {
                 const float c = cc[(size_t)i * rw + j];

@@ -20,6 +20,11 @@
  *   FGS         = num_iter x (row tridiagonal solve, column tridiagonal solve), lambda *= 0.25
  *                 per iteration; weights w = exp(-sqrt(|dI|^2)/sigma) between 4-neighbours of
  *                 the guide, system (1 + lambda*sum w) u_p - lambda*sum w u_q = f_p (Thomas).
+ *                 Two solvers of that system are restated (fgs_solver): ORC_FGS_THOMAS, the
+ *                 sequential elimination ximgproc runs; ORC_FGS_PCR, parallel cyclic reduction
+ *                 (the engine's default: every stage is data-parallel).  Both solve the same
+ *                 diagonally dominant system; they differ only in float rounding (tests pin PCR
+ *                 against THOMAS at <= 1 int16 level on the WLS output).
  *   output      = saturate_cast<short>(FGS(conf * d) / FGS(conf)) (0 where FGS(conf) == 0)
  *                 inside the valid ROI, 16*(minDisparity-1) outside.
  *   ROI (SGBM)  = (max(0, minD+numD), 0, W - that - max(0, -minD), H).
@@ -48,7 +53,10 @@ typedef struct {
     int num_iter;              /* FGS default 3 */
     int roi_x, roi_y, roi_w, roi_h; /* valid ROI of the left disparity map */
     int min_disp;              /* left matcher minDisparity (outside-ROI value 16*(min_disp-1)) */
+    int fgs_solver;            /* ORC_FGS_PCR (default) or ORC_FGS_THOMAS */
 } orc_wls_params;
+
+enum { ORC_FGS_PCR = 0, ORC_FGS_THOMAS = 1 };
 
 /* createDisparityWLSFilter(StereoSGBM) defaults for a W x H left map. */
 void orc_wls_params_for_sgbm(int minDisparity, int numDisparities, int blockSize, int width,
@@ -66,9 +74,13 @@ void orc_wls_confidence(const int16_t* dl, const int16_t* dr, int width, int hei
                         const orc_wls_params* p, float* conf);
 
 /* FastGlobalSmootherFilter(guide, lambda, sigma, attenuation, iters).filter(img) in place;
- * img and guide are w x h (guide row stride gstride bytes). */
+ * img and guide are w x h (guide row stride gstride bytes).  Sequential (Thomas) line solves. */
 void orc_fgs_filter_f32(const uint8_t* guide, size_t gstride, int w, int h, double lambda,
                         double sigma_color, double lambda_attenuation, int num_iter, float* img);
+/* The same filter with the line solver chosen by `solver` (ORC_FGS_*). */
+void orc_fgs_filter_f32_ex(const uint8_t* guide, size_t gstride, int w, int h, double lambda,
+                           double sigma_color, double lambda_attenuation, int num_iter, int solver,
+                           float* img);
 
 /* DisparityWLSFilter::filter(dl, guide, out, dr): out W*H int16; conf_out (nullable) W*H. */
 void orc_wls_filter(const int16_t* dl, const int16_t* dr, const uint8_t* guide, size_t gstride,

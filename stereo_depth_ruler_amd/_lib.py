@@ -42,7 +42,11 @@ class WlsParams(ctypes.Structure):
                 ("roll_off", ctypes.c_float), ("lambda_attenuation", ctypes.c_double),
                 ("num_iter", ctypes.c_int), ("left_offset", ctypes.c_int),
                 ("right_offset", ctypes.c_int), ("top_offset", ctypes.c_int),
-                ("bottom_offset", ctypes.c_int), ("min_disp", ctypes.c_int)]
+                ("bottom_offset", ctypes.c_int), ("min_disp", ctypes.c_int),
+                ("fgs_solver", ctypes.c_int)]
+
+
+FGS_PCR, FGS_THOMAS = 0, 1  # SDR_FGS_* (sdr_wls_params.fgs_solver)
 
 
 _lib = None
@@ -124,7 +128,7 @@ SIGNATURES = [
     ("sdr_pcd_header", _i, [_i, _i, _c.c_char_p, _sz]),
     ("sdr_write_pcd_binary", _i, [_c.c_char_p, _vp, _i, _i]),
     ("sdr_fgs_filter_device", _i, [_vp, _sz, _i, _i, _c.c_double, _c.c_double, _c.c_double, _i,
-                                   _vp, _i, _vp]),
+                                   _vp, _i, _i, _vp]),
     ("sdr_colormap_lut", _i, [_i, _vp]),
     ("sdr_display_create", _i, [_i, _c.POINTER(_vp)]),
     ("sdr_display_destroy", _i, [_vp]),

@@ -13,18 +13,25 @@
 //   k_wls_conf     left discontinuity (inline) + discontinuity-aware LR check -> confidence
 //                  x255 (full map for getConfidenceMap) and the two FGS inputs conf*d, conf,
 //                  compacted to the ROI
-//   k_fgs_sweep   one FGS pass (rows or columns) = one tridiagonal Thomas solve per line for
-//                  BOTH inputs at once (the elimination coefficients depend only on the guide
-//                  and lambda).  Lane = line over k-major data (coalesced), loads PF samples
-//                  ahead in registers, so a step costs the t-recurrence's division latency
-//   k_transpose2   LDS-tiled transposes between the row pass's column-major copies and the
-//                  column pass's row-major images; k_fgs_weights builds both weight layouts once
+//   k_fgs_pcr      one FGS pass (rows or columns), the default solver (SDR_FGS_PCR): every line's
+//                  tridiagonal system solved by parallel cyclic reduction in LDS, a 256-thread
+//                  workgroup per line (or per G short lines), both right-hand sides at once, the
+//                  diagonal carried as the row sum (oracle/wls_oracle.c fgs_line_pcr: every term
+//                  non-negative, ~200x closer to the exact solution than the sequential sweep);
+//                  rows and columns are both read in place from the row-major images
+//   k_fgs_sweep    one FGS pass with the sequential solver (SDR_FGS_THOMAS, ximgproc's own
+//                  elimination order, bit-exact with oracle/wls_oracle.c fgs_line): lane = line
+//                  over k-major data, PF samples loaded ahead in registers; one lane per line
+//                  leaves the chip nearly idle (6-9 waves at 640x360: ~112 us per pass)
+//   k_transpose2   LDS-tiled transposes between the sweep's column-major copies and the row-major
+//                  images; k_fgs_weights builds the weights once per frame
 //   k_wls_final    FGS(conf*d) / FGS(conf) -> saturate_cast<short>, 16*(min_disp-1) outside ROI
 #include "../../include/sdr/sdr.h"
 #include "sdr_internal.hpp"
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -254,11 +261,155 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const f
     }
 }
 
-// FGS weights of one guide (per frame): ChT (column-major, for the row pass: weight between
-// (i, j) and (i, j+1) at j*h + i) and Cv (row-major, for the column pass: (i, j)-(i+1, j) at i*w + j)
+// FGS line solves by parallel cyclic reduction (the default solver), in the operation order of
+// oracle/wls_oracle.c fgs_line_pcr.  A 256-thread workgroup owns G lines of n samples of one
+// frame (G = 1 for long lines); equation e = g*n + k of the block lives in registers of thread
+// e mod 256 (slot e / 256), so a thread keeps its equations' (a, c, e, b, d0, d1) across the
+// log2(n) stages and only publishes what its neighbours read:
+//   X[e] = {row sum, 1/b, d0, d1} (one 16-byte LDS word), A[e] = a, Cc[e] = c
+// Stage s reads X and A of e - s, X and Cc of e + s (zeros past the line's ends), then every
+// equation is rewritten at once; two barriers per stage.  The images are read and written in
+// place in their row-major layout: for rows (lines = rows) a block's loads are whole rows, for
+// columns (lines = columns) G adjacent columns per row; the loads and stores go through LDS with
+// consecutive threads on consecutive addresses.  Weights Cw: same layout as the images (Ch for
+// rows, Cv for columns, 0 on each line's last sample).
+constexpr int kPcrThreads = 256;
+constexpr int kPcrMaxN = 4096;  // samples per block (G * n): 16 equations per thread
+
+template <int EPT, bool TWO>
+__global__ __launch_bounds__(kPcrThreads) void k_fgs_pcr(float* U0, float* U1, const float* __restrict__ Cw,
+                                                         int w, int h, size_t fstride, int rows, int G,
+                                                         float lam) {
+    extern __shared__ float4 pcr_smem[];
+    const int n = rows ? w : h;
+    const int nlines = rows ? h : w;
+    const int N = G * n;
+    float4* X = pcr_smem;               // [N] {row sum, 1/b, d0, d1}
+    float* A = (float*)(X + N);         // [N] a (sub-diagonal); the weights during the load
+    float* Cc = A + N;                  // [N] c (super-diagonal)
+    const int tid = threadIdx.x;
+    const int l0 = blockIdx.x * G;
+    const size_t fo = (size_t)blockIdx.y * fstride;
+    // ---- coalesced load into LDS: weight -> A[e], rhs -> X[e].z/.w ----
+    for (int idx = tid; idx < N; idx += kPcrThreads) {
+        int g, k;
+        size_t off;
+        if (rows) {
+            g = idx / n;
+            k = idx - g * n;
+            off = (size_t)(l0 + g) * w + k;
+        } else {
+            k = idx / G;
+            g = idx - k * G;
+            off = (size_t)k * w + l0 + g;
+        }
+        const int e = g * n + k;
+        float cw = 0.0f, r0 = 0.0f, r1 = 0.0f;
+        if (l0 + g < nlines) {
+            cw = Cw[fo + off];
+            r0 = U0[fo + off];
+            if constexpr (TWO) r1 = U1[fo + off];
+        }
+        A[e] = cw;
+        X[e] = make_float4(0.0f, 0.0f, r0, r1);
+    }
+    __syncthreads();
+    float a[EPT], c[EPT], rs[EPT], b[EPT], d0[EPT], d1[EPT];
+    int kk[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+        const int e = tid + j * kPcrThreads;
+        kk[j] = 0;
+        a[j] = c[j] = 0.0f;
+        rs[j] = b[j] = 1.0f;
+        d0[j] = d1[j] = 0.0f;
+        if (e < N) {
+            const int k = e - (e / n) * n;
+            kk[j] = k;
+            c[j] = lam * A[e];
+            a[j] = k > 0 ? lam * A[e - 1] : 0.0f;
+            rs[j] = 1.0f;
+            b[j] = (1.0f - a[j]) - c[j];
+            d0[j] = X[e].z;
+            d1[j] = X[e].w;
+        }
+    }
+    __syncthreads();
+    for (int s = 1; s < n; s <<= 1) {
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int e = tid + j * kPcrThreads;
+            if (e < N) {
+                X[e] = make_float4(rs[j], 1.0f / b[j], d0[j], d1[j]);
+                A[e] = a[j];
+                Cc[e] = c[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < EPT; j++) {
+            const int e = tid + j * kPcrThreads;
+            if (e < N) {
+                float4 xm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), xp = xm;
+                float am = 0.0f, cp = 0.0f;
+                if (kk[j] >= s) {
+                    xm = X[e - s];
+                    am = A[e - s];
+                }
+                if (kk[j] + s < n) {
+                    xp = X[e + s];
+                    cp = Cc[e + s];
+                }
+                const float k1 = a[j] * xm.y;
+                const float k2 = c[j] * xp.y;
+                const float na = -(am * k1);
+                const float nc = -(cp * k2);
+                const float ne = (rs[j] - xm.x * k1) - xp.x * k2;
+                b[j] = (ne - na) - nc;
+                a[j] = na;
+                c[j] = nc;
+                rs[j] = ne;
+                d0[j] = (d0[j] - xm.z * k1) - xp.z * k2;
+                if constexpr (TWO) d1[j] = (d1[j] - xm.w * k1) - xp.w * k2;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- decoupled: u = d / b, staged in LDS for the coalesced store ----
+#pragma unroll
+    for (int j = 0; j < EPT; j++) {
+        const int e = tid + j * kPcrThreads;
+        if (e < N) {
+            X[e].z = d0[j] / b[j];
+            if constexpr (TWO) X[e].w = d1[j] / b[j];
+        }
+    }
+    __syncthreads();
+    for (int idx = tid; idx < N; idx += kPcrThreads) {
+        int g, k;
+        size_t off;
+        if (rows) {
+            g = idx / n;
+            k = idx - g * n;
+            off = (size_t)(l0 + g) * w + k;
+        } else {
+            k = idx / G;
+            g = idx - k * G;
+            off = (size_t)k * w + l0 + g;
+        }
+        if (l0 + g >= nlines) continue;
+        const float4 x = X[g * n + k];
+        U0[fo + off] = x.z;
+        if constexpr (TWO) U1[fo + off] = x.w;
+    }
+}
+
+// FGS weights of one guide (per frame): Ch (weight between (i, j) and (i, j+1): column-major at
+// j*h + i for the sequential sweep, row-major at i*w + j for k_fgs_pcr) and Cv (row-major:
+// (i, j)-(i+1, j) at i*w + j)
 __global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__ guide, size_t gstride,
                                                      size_t gfstride, const float* __restrict__ lut,
-                                                     int w, int h, float* __restrict__ ChT,
+                                                     int w, int h, int ch_rowmajor, float* __restrict__ ChT,
                                                      float* __restrict__ Cv) {
     const int j = blockIdx.x * 64 + (threadIdx.x & 63);
     const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
@@ -275,7 +426,7 @@ __global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__
         const int d = v - g[gstride];
         cv = lut[d * d];
     }
-    ChT[fo + (size_t)j * h + i] = ch;
+    ChT[fo + (ch_rowmajor ? (size_t)i * w + j : (size_t)j * h + i)] = ch;
     Cv[fo + (size_t)i * w + j] = cv;
 }
 
@@ -340,24 +491,64 @@ static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const flo
     else hipLaunchKernelGGL((k_fgs_sweep<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
 }
 
-static void launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
-                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
-                       int iters, const FgsScratch& s, hipStream_t st) {
+// k_fgs_pcr instance for G*n samples per block (EPT equations per thread)
+template <bool TWO>
+static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F, int rows,
+                      float lam, hipStream_t st) {
+    const int n = rows ? w : h, nlines = rows ? h : w;
+    if (n > kPcrMaxN) return -1;
+    // short lines: G per block so that a block holds up to 768 samples (3 per thread)
+    const int G = std::max(1, std::min(nlines, 768 / n));
+    const int N = G * n;
+    const int need = (N + kPcrThreads - 1) / kPcrThreads;
+    const dim3 grid((nlines + G - 1) / G, F), blk(kPcrThreads);
+    const size_t lds = (size_t)N * 24;
     const size_t fs = (size_t)w * h;
+#define SDR_PCR(E)                                                                                     \
+    if (need <= E) {                                                                                   \
+        hipLaunchKernelGGL((k_fgs_pcr<E, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam); \
+        return 0;                                                                                      \
+    }
+    SDR_PCR(1) SDR_PCR(2) SDR_PCR(3) SDR_PCR(4) SDR_PCR(6) SDR_PCR(8) SDR_PCR(12) SDR_PCR(16)
+#undef SDR_PCR
+    return -1;
+}
+
+// FastGlobalSmootherFilter::filter on R0 (and R1 when non-null: a second right-hand side of the
+// same systems), row-major w x h per frame, F frames with per-frame guides, in place.
+//   SDR_FGS_PCR:    weights (Ch, Cv row-major), then per iteration k_fgs_pcr over the rows and
+//                   over the columns of the images themselves (2 launches per iteration)
+//   SDR_FGS_THOMAS: weights (ChT column-major, Cv), then per iteration transpose -> row sweep ->
+//                   transpose back -> column sweep (4 launches per iteration)
+// Scratch (each F*w*h floats): A, B (column-major copies, THOMAS), T (THOMAS), ChT, Cv (weights).
+static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
+                      float* R0, float* R1, int w, int h, int F, double lambda, double att,
+                      int iters, int solver, const FgsScratch& s, hipStream_t st) {
+    const size_t fs = (size_t)w * h;
+    const bool pcr = solver == SDR_FGS_PCR;
     hipLaunchKernelGGL(k_fgs_weights, dim3((w + 63) / 64, (h + 3) / 4, F), dim3(256), 0, st, guide,
-                       gstride, gfstride, lut, w, h, s.ChT, s.Cv);
+                       gstride, gfstride, lut, w, h, pcr ? 1 : 0, s.ChT, s.Cv);
     const dim3 t_rm((w + 63) / 64, (h + 63) / 64, F), t_cm((h + 63) / 64, (w + 63) / 64, F);
     float lam = (float)lambda;
     const float fa = (float)att;
     for (int it = 0; it < iters; it++) {
-        // row pass on column-major copies (lines = rows, k = column)
-        hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
-        fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
-        hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
-        // column pass in place on the row-major images (lines = columns, k = row)
-        fgs_sweep(dim3((w + 63) / 64, F), st, R0, R1, s.Cv, s.T, w, h, fs, lam);
+        if (pcr) {
+            const int e1 = R1 ? launch_pcr<true>(R0, R1, s.ChT, w, h, F, 1, lam, st)
+                              : launch_pcr<false>(R0, R1, s.ChT, w, h, F, 1, lam, st);
+            const int e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
+                              : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
+            if (e1 || e2) return -1;
+        } else {
+            // row pass on column-major copies (lines = rows, k = column)
+            hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
+            fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
+            hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
+            // column pass in place on the row-major images (lines = columns, k = row)
+            fgs_sweep(dim3((w + 63) / 64, F), st, R0, R1, s.Cv, s.T, w, h, fs, lam);
+        }
         lam = lam * fa;  // FastGlobalSmootherFilterImpl::filter: lambda *= lambda_attenuation
     }
+    return 0;
 }
 
 // ComputeLUT_ParBody: LUT[i] = -exp(-sqrt((float)i) / sigmaColor), float math on the host
@@ -393,6 +584,8 @@ namespace {
 int check_wls_params(const sdr_wls_params& p) {
     if (!(p.lambda >= 0.0) || !(p.sigma_color >= 0.0) || p.num_iter < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
+    if (p.fgs_solver != SDR_FGS_PCR && p.fgs_solver != SDR_FGS_THOMAS)
+        return sdr::set_error(SDR_ERR_ARG, "fgs_solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
     if (p.depth_discontinuity_radius < 0 || p.left_offset < 0 || p.right_offset < 0 ||
         p.top_offset < 0 || p.bottom_offset < 0)
         return sdr::set_error(SDR_ERR_ARG, "negative WLS radius or offset");
@@ -437,6 +630,7 @@ void sdr_wls_params_for_sgbm(sdr_sgbm_params* m, sdr_wls_params* p) {
     p->top_offset = 0;
     p->bottom_offset = 0;
     p->min_disp = m->minDisparity;
+    p->fgs_solver = SDR_FGS_PCR;
 }
 
 int sdr_wls_create(const sdr_wls_params* p, int device, sdr_wls** out) {
@@ -530,6 +724,9 @@ int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, cons
     g.fill = 16 * (p.min_disp - 1);
     const size_t px = (size_t)W * H;
     const bool roi = g.rw > 0 && g.rh > 0;
+    if (roi && p.fgs_solver == SDR_FGS_PCR && (g.rw > sdr::kPcrMaxN || g.rh > sdr::kPcrMaxN))
+        return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
+                                            "(use SDR_FGS_THOMAS for larger ROIs)");
     const size_t cpx = roi ? (size_t)g.rw * g.rh : 0;
     int rc;
     const float* lut = nullptr;
@@ -551,8 +748,10 @@ int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, cons
         const uint8_t* g0 = guide + (size_t)g.ry * gstride + g.rx;
         const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
                                  (float*)h->Cv.p};
-        sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
-                        p.lambda_attenuation, p.num_iter, fs, st);
+        if (sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
+                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st))
+            return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
+                                                "(use SDR_FGS_THOMAS for larger ROIs)");
     }
     hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out);
     WLS_HIP(hipGetLastError());
@@ -588,12 +787,17 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8
 
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, double lambda,
                           double sigma, double att, int iters, float* d_img, int nimg,
-                          void* stream) {
+                          int solver, void* stream) {
     if (!d_guide || !d_img) return sdr::set_error(SDR_ERR_ARG, "null argument");
     if (w <= 0 || h <= 0 || nimg <= 0 || gstride < (size_t)w)
         return sdr::set_error(SDR_ERR_ARG, "bad size/stride");
     if (!(lambda >= 0.0) || !(sigma >= 0.0) || iters < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
+    if (solver != SDR_FGS_PCR && solver != SDR_FGS_THOMAS)
+        return sdr::set_error(SDR_ERR_ARG, "solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
+    if (solver == SDR_FGS_PCR && (w > sdr::kPcrMaxN || h > sdr::kPcrMaxN))
+        return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
+                                            "(use SDR_FGS_THOMAS for larger images)");
     hipStream_t st = (hipStream_t)stream;
     std::vector<float> lut;
     sdr::fgs_lut_host(sigma, &lut);
@@ -608,8 +812,8 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
     // images are filtered in pairs (two right-hand sides of one system per line)
     for (int i = 0; i < nimg; i += 2) {
         const int m = nimg - i >= 2 ? 2 : 1;
-        sdr::launch_fgs(d_guide, gstride, 0, dlut, d_img + i * px, m == 2 ? d_img + (i + 1) * px : nullptr,
-                        w, h, 1, lambda, att, iters, fs, st);
+        (void)sdr::launch_fgs(d_guide, gstride, 0, dlut, d_img + i * px, m == 2 ? d_img + (i + 1) * px : nullptr,
+                              w, h, 1, lambda, att, iters, solver, fs, st);
     }
     WLS_HIP(hipGetLastError());
     WLS_HIP(hipFreeAsync(dlut, st));

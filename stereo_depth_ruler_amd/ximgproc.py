@@ -17,7 +17,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import SDRError, WlsParams, check, lib
+from ._lib import FGS_PCR, FGS_THOMAS, SDRError, WlsParams, check, lib  # noqa: F401
 from .sgbm import StereoSGBM, _cstream, _is_cuda, createRightMatcher, torch  # noqa: F401
 
 
@@ -55,6 +55,9 @@ class DisparityWLSFilter:
     def setLRCthresh(self, v): self._set("lrc_thresh", int(v))
     def getDepthDiscontinuityRadius(self): return self._p.depth_discontinuity_radius
     def setDepthDiscontinuityRadius(self, v): self._set("depth_discontinuity_radius", int(v))
+    # engine extension: the FGS line solver (FGS_PCR, the default, or FGS_THOMAS: sdr.h)
+    def getFgsSolver(self): return self._p.fgs_solver
+    def setFgsSolver(self, v): self._set("fgs_solver", int(v))
 
     def params(self) -> WlsParams:
         p = WlsParams()
@@ -142,15 +145,16 @@ def createDisparityWLSFilterGeneric(use_confidence: bool, device: int = 0) -> Di
     confidence-based variant (use_confidence=True) is implemented."""
     if not use_confidence:
         raise SDRError(-1, "createDisparityWLSFilterGeneric(false) is not implemented")
-    p = WlsParams(8000.0, 1.5, 24, 5, 0.001, 0.25, 3, 0, 0, 0, 0, 0)
+    p = WlsParams(8000.0, 1.5, 24, 5, 0.001, 0.25, 3, 0, 0, 0, 0, 0, FGS_PCR)
     return DisparityWLSFilter(p, device)
 
 
 def fastGlobalSmootherFilter(guide, src, lambda_, sigma_color, lambda_attenuation=0.25,
-                             num_iter=3):
+                             num_iter=3, solver=FGS_PCR):
     """cv::ximgproc::fastGlobalSmootherFilter on a float32 (H, W) image (or (N, H, W) stack
     sharing one guide) with an 8-bit gray guide.  torch CUDA tensors are filtered on the current
-    stream; numpy arrays go through the current CUDA device."""
+    stream; numpy arrays go through the current CUDA device.  solver: FGS_PCR (default) or
+    FGS_THOMAS (ximgproc's sequential elimination, bit for bit; include/sdr/sdr.h)."""
     if torch is None:
         raise SDRError(-6, "fastGlobalSmootherFilter needs torch for device memory")
     host = not _is_cuda(src)
@@ -167,6 +171,6 @@ def fastGlobalSmootherFilter(guide, src, lambda_, sigma_color, lambda_attenuatio
         raise SDRError(-1, "guide and src must have the same (H, W) size")
     check(lib().sdr_fgs_filter_device(g.data_ptr(), w, w, h, float(lambda_), float(sigma_color),
                                       float(lambda_attenuation), int(num_iter), s.data_ptr(), n,
-                                      _cstream(dev.index)))
+                                      int(solver), _cstream(dev.index)))
     out = s[0] if squeeze else s
     return out.cpu().numpy() if host else out

@@ -21,7 +21,7 @@ def declared_functions():
 
 
 def test_library_loads():
-    assert _lib.lib().sdr_abi_version() == 2
+    assert _lib.lib().sdr_abi_version() == 3
 
 
 def test_every_declared_symbol_exported():

@@ -3,8 +3,11 @@
 
 The kernels evaluate every float operation in the oracle's order with contraction off, IEEE
 division and the oracle's host-computed weight table, so the filtered int16 map, the confidence
-map and raw FGS output are compared BIT FOR BIT.  Parity of the oracle itself against
-opencv_contrib is unpinned (no OpenCV in this image, no fixtures in the reference): see
+map and raw FGS output are compared BIT FOR BIT -- for both line solvers: SDR_FGS_THOMAS
+(ximgproc's sequential elimination) against the oracle's fgs_line, SDR_FGS_PCR (the default,
+parallel cyclic reduction) against its fgs_line_pcr.  The two solvers themselves are compared at
+the north-star tolerance (<= 1 int16 level of the WLS output) in
+test_pcr_within_one_level_of_thomas.  Parity of the oracle itself against opencv_contrib is unpinned (no OpenCV in this image, no fixtures in the reference): see
 oracle/wls_oracle.h and tests/test_oracle_wls.py for how the restatement is pinned.
 """
 import numpy as np
@@ -18,7 +21,7 @@ import stereo_depth_ruler_amd as sdr  # noqa: E402
 from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
 from stereo_depth_ruler_amd.ximgproc import (  # noqa: E402
     DisparityWLSFilter, createDisparityWLSFilter, fastGlobalSmootherFilter)
-from stereo_depth_ruler_amd._lib import WlsParams  # noqa: E402
+from stereo_depth_ruler_amd._lib import FGS_PCR, FGS_THOMAS, WlsParams  # noqa: E402
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -34,7 +37,7 @@ def bits(a):
 def wls_from_oracle_params(q) -> DisparityWLSFilter:
     """A device filter with exactly the oracle's parameters (ROI given as offsets)."""
     p = WlsParams(q.lambda_, q.sigma_color, q.lrc_thresh, q.depth_disc_radius, q.roll_off,
-                  q.lambda_attenuation, q.num_iter, q.roi_x, 0, q.roi_y, 0, q.min_disp)
+                  q.lambda_attenuation, q.num_iter, q.roi_x, 0, q.roi_y, 0, q.min_disp, q.fgs_solver)
     return p
 
 
@@ -45,27 +48,40 @@ def make_filter(q, W, H):
     return DisparityWLSFilter(p)
 
 
+SOLVERS = [FGS_PCR, FGS_THOMAS]
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("shape", [(1, 1), (1, 37), (29, 1), (40, 61), (64, 64), (65, 129),
-                                   (97, 130), (200, 333)])
+                                   (97, 130), (200, 333), (3, 1000), (700, 5)])
 @pytest.mark.parametrize("lam,sigma", [(8000.0, 1.1), (50.0, 5.0)])
-def test_fgs_bit_exact(oracle, shape, lam, sigma):
+def test_fgs_bit_exact(oracle, shape, lam, sigma, solver):
     rng = np.random.default_rng(sum(shape))
     g = rng.integers(0, 256, shape).astype(np.uint8)
     g[: shape[0] // 2] //= 8
     x = (rng.random(shape) * 1000).astype(np.float32)
-    ref = oracle.fgs_filter(g, x, lam, sigma)
-    got = fastGlobalSmootherFilter(g, x, lam, sigma)
+    ref = oracle.fgs_filter(g, x, lam, sigma, solver=solver)
+    got = fastGlobalSmootherFilter(g, x, lam, sigma, solver=solver)
     assert np.array_equal(bits(got), bits(ref))
 
 
-def test_fgs_stack_and_iterations(oracle):
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_fgs_stack_and_iterations(oracle, solver):
     rng = np.random.default_rng(5)
     g = rng.integers(0, 256, (70, 90)).astype(np.uint8)
     xs = (rng.random((3, 70, 90)) * 300).astype(np.float32)
-    got = fastGlobalSmootherFilter(g, xs, 8000.0, 1.1, 0.25, 5)
+    got = fastGlobalSmootherFilter(g, xs, 8000.0, 1.1, 0.25, 5, solver=solver)
     for i in range(3):
-        ref = oracle.fgs_filter(g, xs[i], 8000.0, 1.1, 0.25, 5)
+        ref = oracle.fgs_filter(g, xs[i], 8000.0, 1.1, 0.25, 5, solver=solver)
         assert np.array_equal(bits(got[i]), bits(ref))
+
+
+def test_pcr_line_limit():
+    g = np.zeros((2, 4097), np.uint8)
+    x = np.ones((2, 4097), np.float32)
+    with pytest.raises(sdr.SDRError):
+        fastGlobalSmootherFilter(g, x, 8000.0, 1.1, solver=FGS_PCR)
+    assert np.allclose(fastGlobalSmootherFilter(g, x, 8000.0, 1.1, solver=FGS_THOMAS), 1.0, rtol=1e-3)
 
 
 def sgbm_pair_maps(oracle, h, w, numD, seed, minD=0):
@@ -78,10 +94,12 @@ def sgbm_pair_maps(oracle, h, w, numD, seed, minD=0):
     return L, dl, dr
 
 
+@pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("h,w,numD,seed", [(360, 640, 80, 1), (90, 200, 32, 2), (50, 121, 16, 3)])
-def test_wls_filter_bit_exact_on_sgbm_maps(oracle, h, w, numD, seed):
+def test_wls_filter_bit_exact_on_sgbm_maps(oracle, h, w, numD, seed, solver):
     L, dl, dr = sgbm_pair_maps(oracle, h, w, numD, seed)
     q = oracle.wls_params_for_sgbm(0, numD, 5, w, h, 8000.0, 1.1)
+    q.fgs_solver = solver
     ref, ref_conf = oracle.wls_filter(dl, dr, L, q, return_conf=True)
     f = make_filter(q, w, h)
     got = f.filter(dl, L, dr)
@@ -90,7 +108,32 @@ def test_wls_filter_bit_exact_on_sgbm_maps(oracle, h, w, numD, seed):
     assert f.getROI(w, h) == (q.roi_x, q.roi_y, q.roi_w, q.roi_h)
 
 
-def test_wls_params_variants(oracle):
+@pytest.mark.parametrize("seed", [1, 5, 9])
+def test_pcr_within_one_level_of_thomas(oracle, seed):
+    """The default solver against ximgproc's sequential one on the reference's own workload
+    (C0: 640x360 d=80 3WAY left + right matcher maps of a live-loop frame): the north-star
+    tolerance, <= 1 int16 level (1/16 px) everywhere.  Both come from the device."""
+    from stereo_depth_ruler_amd.synthetic import sbs_bgr_color_frame
+    frame = sbs_bgr_color_frame(720, 1280, 80, seed=seed)
+    gl = oracle.resize_area_half(oracle.bgr2gray(frame[:, :1280]))
+    gr = oracle.resize_area_half(oracle.bgr2gray(frame[:, 1280:]))
+    dl = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    dr = oracle.sgbm_compute(gr, gl, oracle.make_params(-79, 80, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+    q = oracle.wls_params_for_sgbm(0, 80, 5, 640, 360, 8000.0, 1.1)
+    f = make_filter(q, 640, 360)
+    f.setFgsSolver(FGS_PCR)
+    pcr = f.filter(dl, gl, dr).astype(np.int32)
+    f.setFgsSolver(FGS_THOMAS)
+    tho = f.filter(dl, gl, dr).astype(np.int32)
+    d = np.abs(pcr - tho)
+    same = float((d == 0).mean())
+    print(f"seed {seed}: max |PCR - THOMAS| = {d.max()} level(s), {100 * same:.3f} % bit-identical")
+    assert d.max() <= 1
+    assert same > 0.999
+
+
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_wls_params_variants(oracle, solver):
     """radius, LRC threshold, lambda/sigma, minDisparity < 0 (both ROI offsets), ROI y offsets."""
     rng = np.random.default_rng(9)
     h, w = 77, 190
@@ -104,6 +147,7 @@ def test_wls_params_variants(oracle):
         q = oracle.wls_params_for_sgbm(minD, numD, bs, w, h, lam, sig)
         q.lrc_thresh = thr
         q.roi_y, q.roi_h = 3, h - 7
+        q.fgs_solver = solver
         ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)
         f = make_filter(q, w, h)
         got = f.filter(dl, g, dr)
@@ -111,7 +155,8 @@ def test_wls_params_variants(oracle):
         assert np.array_equal(got, ref), (minD, numD, bs)
 
 
-def test_wls_edge_cases(oracle):
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_wls_edge_cases(oracle, solver):
     h, w = 40, 120
     g = np.random.default_rng(1).integers(0, 256, (h, w)).astype(np.uint8)
     cases = [
@@ -122,6 +167,7 @@ def test_wls_edge_cases(oracle):
          np.random.default_rng(3).integers(-32768, 32767, (h, w)).astype(np.int16)),  # extremes
     ]
     q = oracle.wls_params_for_sgbm(0, 32, 5, w, h, 8000.0, 1.1)
+    q.fgs_solver = solver
     f = make_filter(q, w, h)
     for dl, dr in cases:
         ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)

@@ -21,33 +21,39 @@ def test_lut_matches_formula(oracle):
     assert lut[0] == -1.0
 
 
-@pytest.mark.parametrize("shape", [(1, 1), (1, 37), (29, 1), (40, 61), (97, 130)])
+@pytest.mark.parametrize("shape", [(1, 1), (1, 37), (29, 1), (40, 61), (97, 130), (5, 700)])
 @pytest.mark.parametrize("lam,sigma", [(8000.0, 1.1), (50.0, 5.0), (0.5, 20.0)])
 def test_fgs_matches_float64_restatement(oracle, shape, lam, sigma):
+    """Both line solvers against float64 banded solves.  The sequential sweep (ximgproc's) loses
+    ~lambda * 2^-24 relative at lambda = 8000 (its elimination denominators cancel); the PCR
+    solver carries each diagonal as a row sum of non-negative terms and stays within a few ulp."""
     rng = np.random.default_rng(sum(shape))
     g = rng.integers(0, 256, shape).astype(np.uint8)
     g[: shape[0] // 2] //= 8  # flat and textured halves
     x = (rng.random(shape) * 1000).astype(np.float32)
-    got = oracle.fgs_filter(g, x, lam, sigma)
     ref = N.fgs_filter(g, x, lam, sigma)
-    assert np.allclose(got, ref, rtol=2e-4, atol=2e-2 * max(1.0, float(np.abs(ref).max()) * 1e-3))
+    tho = oracle.fgs_filter(g, x, lam, sigma, solver=oracle.FGS_THOMAS)
+    assert np.allclose(tho, ref, rtol=2e-4, atol=2e-2 * max(1.0, float(np.abs(ref).max()) * 1e-3))
+    pcr = oracle.fgs_filter(g, x, lam, sigma, solver=oracle.FGS_PCR)
+    assert np.allclose(pcr, ref, rtol=4e-6, atol=1e-4)
 
 
-def test_fgs_properties(oracle):
+@pytest.mark.parametrize("solver", [0, 1])
+def test_fgs_properties(oracle, solver):
     rng = np.random.default_rng(3)
     g = rng.integers(0, 256, (64, 80)).astype(np.uint8)
     x = (rng.random((64, 80)) * 500).astype(np.float32)
-    y = oracle.fgs_filter(g, x, 8000.0, 1.1)
+    y = oracle.fgs_filter(g, x, 8000.0, 1.1, solver=solver)
     assert abs(float(y.sum(dtype=np.float64)) - float(x.sum(dtype=np.float64))) < 1e-4 * float(x.sum())
-    assert np.array_equal(oracle.fgs_filter(g, x, 0.0, 1.1), x)               # lam = 0: identity
+    assert np.array_equal(oracle.fgs_filter(g, x, 0.0, 1.1, solver=solver), x)   # lam = 0: identity
     c = np.full((64, 80), 37.0, np.float32)
     # fixed point; f32 sweeps at condition ~lambda lose ~lambda * 2^-24 relative
-    assert np.allclose(oracle.fgs_filter(g, c, 8000.0, 1.1), 37.0, rtol=5e-4)
+    assert np.allclose(oracle.fgs_filter(g, c, 8000.0, 1.1, solver=solver), 37.0, rtol=5e-4)
     # edge-aware: a step in the guide keeps a step in the image
     g2 = np.zeros((32, 64), np.uint8)
     g2[:, 32:] = 200
     s = np.where(np.arange(64)[None, :] < 32, 0.0, 100.0).repeat(32, 0).astype(np.float32)
-    out = oracle.fgs_filter(g2, s, 8000.0, 1.1)
+    out = oracle.fgs_filter(g2, s, 8000.0, 1.1, solver=solver)
     assert out[:, :31].max() < 1.0 and out[:, 33:].min() > 99.0
 
 

@@ -276,6 +276,15 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
                                     const uint8_t* d_small_left, const uint8_t* d_small_right,
                                     int width, int height, int nframes, float* d_out,
                                     int16_t* d_filtered, float* d_conf);
+/* The reference's per-frame pair computeDisparity -> computeDepth (stereo_displayer.cpp:161-162,
+ * stereo_disparity.cpp:17-39,76-80) in one call: sdr_stereo_class_compute_device plus
+ * reprojectImageTo3D(d_out, Q, handleMissing = false) -> d_xyz float32x3 [F][h][w][3], fused into
+ * the WLS filter's last kernel when wls != NULL. */
+int sdr_stereo_class_depth_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                                  const uint8_t* d_small_left, const uint8_t* d_small_right,
+                                  int width, int height, int nframes, float* d_out,
+                                  int16_t* d_filtered, float* d_conf, const double Q[16],
+                                  float* d_xyz);
 
 /* ---- point-cloud emit after the path, point_cloud/src/pcd_write.cpp ----
  * Points are pcl::PointXYZRGB as savePCDFileBinary lays them out: 16-byte records

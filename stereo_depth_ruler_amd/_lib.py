@@ -122,6 +122,8 @@ SIGNATURES = [
     ("sdr_rectify_device", _i, [_vp, _vp, _vp, _sz, _sz, _i, _i, _vp, _vp, _sz, _sz]),
     ("sdr_rectify_sbs_device", _i, [_vp, _vp, _sz, _sz, _i, _vp, _vp, _vp, _vp]),
     ("sdr_stereo_class_compute_device", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    ("sdr_stereo_class_depth_device", _i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp,
+                                           _c.POINTER(_c.c_double), _vp]),
     ("sdr_xyz_to_cloud_device", _i, [_vp, _vp, _sz, _sz, _i, _i, _i, _vp, _vp]),
     ("sdr_voxel_grid_device", _i, [_vp, _i, _c.c_float, _c.c_float, _c.c_float, _vp,
                                    _c.POINTER(_i), _c.POINTER(_i), _vp]),

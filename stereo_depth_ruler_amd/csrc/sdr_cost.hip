@@ -145,7 +145,7 @@ size_t cost_sink_bytes(const Geometry& g) { return (size_t)(g.W1 + 64) * g.D * 2
 bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.SH2 <= 5 && g.D <= 256; }
 
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st) {
-    if (a.row_end <= a.row_begin) return;
+    if (a.row_end <= a.row_begin && a.naux == 0) return;
     if (a.pl.cn == 3) return launch_cost_cn3(g, a, F, st);
     const int NR = 2 * g.SH2 + 1;
     const bool k2 = g.D > 128;

@@ -317,18 +317,34 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     const int gx = gridDim.x, gy = gridDim.y;
     const int l = xcd_block(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), gx * gy * gridDim.z);
     const int bx = l % gx, by = (l / gx) % gy, f = l / (gx * gy);
-    const int ty0 = a.row_begin + by * a.TY;
-    const int ty1 = min(ty0 + a.TY, a.row_end);
+    // row bands [0, gy - naux) of the frame; the last naux bands are the 3WAY stripe starts
+    const int nmain = gy - a.naux;
+    CostArgs aa = a;
+    int ty0, ty1;
+    if (by < nmain) {
+        ty0 = a.row_begin + by * a.TY;
+        ty1 = min(ty0 + a.TY, a.row_end);
+    } else {
+        const CostAux& x = a.aux[by - nmain];
+        aa.out = x.out;
+        aa.out_fstride = a.aux_fstride;
+        aa.out_row0 = x.row0;
+        aa.s0 = x.s0;
+        aa.ylim = x.ylim;
+        aa.hh_bottom = 0;
+        ty0 = x.row0;
+        ty1 = x.row0 + x.rows;
+    }
     if (ty0 >= ty1) return;
     const int bx0 = bx * Cfg::BCOLS;
-    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, CN, true>(g, a, lds, bx, f, ty0, ty1);
-    else cost_block<NR, K, CN, false>(g, a, lds, bx, f, ty0, ty1);
+    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, CN, true>(g, aa, lds, bx, f, ty0, ty1);
+    else cost_block<NR, K, CN, false>(g, aa, lds, bx, f, ty0, ty1);
 }
 
 template <int NR, int K, int CN>
 static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) {
     using Cfg = CostCfg<NR, K, CN>;
-    const int rows = a.row_end - a.row_begin;
+    const int rows = max(a.row_end - a.row_begin, 0);
     const size_t lds = Cfg::lds_bytes(g.D);
     const int colblocks = (g.W1 + Cfg::BCOLS - 1) / Cfg::BCOLS;
     if (a.TY <= 0) {
@@ -347,7 +363,8 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
         const int bands = max(1, slots / max(1, colblocks * F));
         a.TY = max(4, (rows + bands - 1) / bands);
     }
-    dim3 grid(colblocks, (rows + a.TY - 1) / a.TY, F);
+    if (rows == 0) a.TY = 1;
+    dim3 grid(colblocks, (rows + a.TY - 1) / a.TY + a.naux, F);
     hipLaunchKernelGGL((k_cost<NR, K, CN>), grid, dim3(256), lds, st, g, a);
 }
 

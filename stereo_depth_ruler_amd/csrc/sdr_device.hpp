@@ -7,6 +7,7 @@
 // DPP butterflies + v_permlane{16,32}_swap (all in-register, no LDS).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cfloat>
 #include <stdint.h>
 
 #include <type_traits>
@@ -224,6 +225,40 @@ __device__ __forceinline__ int div_trunc_small(int n, int d) {
     q += (r >= d) ? 1 : 0;
     q -= (r < 0) ? 1 : 0;
     return n < 0 ? -q : q;
+}
+
+
+// ------------------------------------------------------------------------------------------
+// A.12 reprojectImageTo3D of one pixel (sdr_post.hip's kernels, the class path's fused WLS
+// epilogue in sdr_wls.hip): double math, sequential sums from 0, no contraction, Vec3f then
+// *(1.0/h3) rounded to float; handleMissing: Z = 10000 where |d - min(disp)| <= FLT_EPSILON.
+// ------------------------------------------------------------------------------------------
+struct Q16 {
+    double q[16];
+};
+
+__device__ __forceinline__ void reproject_px(const Q16& Q, int x, int y, double d, double mind,
+                                             int hm, float* o) {
+#pragma clang fp contract(off)
+    const double v0 = (double)x, v1 = (double)y;
+    double h[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double s = 0.0;
+        s += Q.q[i * 4 + 0] * v0;
+        s += Q.q[i * 4 + 1] * v1;
+        s += Q.q[i * 4 + 2] * d;
+        s += Q.q[i * 4 + 3] * 1.0;
+        h[i] = s;
+    }
+    const double ia = 1.0 / h[3];
+    const float X = (float)((double)(float)h[0] * ia);
+    const float Y = (float)((double)(float)h[1] * ia);
+    float Z = (float)((double)(float)h[2] * ia);
+    if (hm && fabs(d - mind) <= (double)FLT_EPSILON) Z = 10000.f;
+    o[0] = X;
+    o[1] = Y;
+    o[2] = Z;
 }
 
 }  // namespace sdr

@@ -479,23 +479,21 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     ca.hh_bottom = e.mode == SDR_MODE_HH || e.mode == SDR_MODE_HH4;
     ca.TY = 0;  // sized by launch_cost for one full pass of resident blocks
     ca.sink = (int16_t*)h->sink.p;
-    { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
+    // the 3WAY stripe-start rows are extra row bands of the same launch
+    ca.naux = 0;
+    ca.aux_fstride = aux_fstride;
     for (size_t s = 0; s < stripes.size(); s++) {
         const Stripe& sp = stripes[s];
         if (!sp.aux_rows) continue;
-        sdr::CostArgs xa = ca;
-        xa.out = Caux + s * (size_t)amax * g.W1 * g.D;
-        xa.out_fstride = aux_fstride;
-        xa.out_row0 = sp.s0;
-        xa.row_begin = sp.s0;
-        xa.row_end = sp.s0 + sp.aux_rows;
-        xa.s0 = sp.s0;
-        xa.ylim = sp.ylim;
-        xa.hh_bottom = 0;
-        xa.TY = sp.aux_rows;
-        KTimer kt(h, SDR_KERNEL_COST);
-        sdr::launch_cost(g, xa, F, st);
+        if (ca.naux == sdr::kMaxCostAux) return fail(SDR_ERR_ARG, "too many 3WAY stripes");
+        sdr::CostAux& x = ca.aux[ca.naux++];
+        x.out = Caux + s * (size_t)amax * g.W1 * g.D;
+        x.row0 = sp.s0;
+        x.rows = sp.aux_rows;
+        x.s0 = sp.s0;
+        x.ylim = sp.ylim;
     }
+    { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));
 
     // k_paths: every direction except the top-to-bottom one, each into its own L buffer (in the
@@ -999,9 +997,13 @@ int sdr_resize_area_half_device(const uint8_t* d_src, int W, int H, size_t strid
     return SDR_OK;
 }
 
-int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
-                                    const uint8_t* sl, const uint8_t* sr, int w2, int h2, int F,
-                                    float* d_out, int16_t* d_filtered, float* d_conf) {
+}  // extern "C"
+
+// StereoDisparity::computeDisparity from the half-size gray pair on the device, and optionally
+// computeDepth (Q, d_xyz non-null) fused into the WLS epilogue.
+static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const uint8_t* sl,
+                         const uint8_t* sr, int w2, int h2, int F, float* d_out,
+                         int16_t* d_filtered, float* d_conf, const double* Q, float* d_xyz) {
     if (!left || !sl || !sr || !d_out) return fail(SDR_ERR_ARG, "null argument");
     if (w2 <= 0 || h2 <= 0 || F <= 0) return fail(SDR_ERR_ARG, "bad size");
     if (right && right->device != left->device) return fail(SDR_ERR_ARG, "matchers on different devices");
@@ -1040,23 +1042,39 @@ int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wl
     }
     if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
     if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
-    const int16_t* res = dl;
     if (wls) {
         // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)
+        // with filtered_disp.convertTo(CV_32F, 1/16) (:34) and computeDepth (:76-80) in its epilogue
         void* ws = sdr_wls_get_stream(wls);
         (void)sdr_wls_set_stream(wls, st);
-        rc = sdr_wls_filter_device(wls, dl, dr, sl, w2, h2, w2, px2, F, dw, d_conf);
+        rc = sdr::wls_filter_enqueue(wls, dl, dr, sl, w2, h2, w2, px2, F, dw, d_conf, d_out, Q, d_xyz);
         (void)sdr_wls_set_stream(wls, ws);
         if (rc) return rc;
-        res = dw;
-    } else if (d_filtered) {
-        SDR_HIP(hipMemcpyAsync(d_filtered, dl, F * px2 * 2, hipMemcpyDeviceToDevice, st));
+    } else {
+        if (d_filtered) SDR_HIP(hipMemcpyAsync(d_filtered, dl, F * px2 * 2, hipMemcpyDeviceToDevice, st));
+        sdr::launch_disp16_to_f32(dl, d_out, F * px2, st);
+        if (d_xyz)
+            sdr::launch_reproject_f32(d_out, w2, h2, w2, px2, Q, 0, nullptr, d_xyz, (size_t)w2 * 3, px2 * 3, F, st);
     }
-    // filtered_disp.convertTo(CV_32F, 1/16) (stereo_disparity.cpp:34)
-    sdr::launch_disp16_to_f32(res, d_out, F * px2, st);
     retire(left);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
+}
+
+extern "C" {
+
+int sdr_stereo_class_compute_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                                    const uint8_t* sl, const uint8_t* sr, int w2, int h2, int F,
+                                    float* d_out, int16_t* d_filtered, float* d_conf) {
+    return class_enqueue(left, right, wls, sl, sr, w2, h2, F, d_out, d_filtered, d_conf, nullptr, nullptr);
+}
+
+int sdr_stereo_class_depth_device(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
+                                  const uint8_t* sl, const uint8_t* sr, int w2, int h2, int F,
+                                  float* d_out, int16_t* d_filtered, float* d_conf,
+                                  const double Q[16], float* d_xyz) {
+    if (!Q || !d_xyz) return fail(SDR_ERR_ARG, "null argument");
+    return class_enqueue(left, right, wls, sl, sr, w2, h2, F, d_out, d_filtered, d_conf, Q, d_xyz);
 }
 
 int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
@@ -1090,8 +1108,7 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     // cvtColor(BGR2GRAY) x2, resize(0.5, INTER_AREA) x2 (stereo_disparity.cpp:19-24)
     sdr::launch_bgr2gray(bgr, W, H, (size_t)W * 3, gray, W, 2, st);
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
-    if ((rc = sdr_stereo_class_compute_device(left, right, wls, small, small + px2, w2, h2, 1, f,
-                                              filt, dconf)))
+    if ((rc = class_enqueue(left, right, wls, small, small + px2, w2, h2, 1, f, filt, dconf, nullptr, nullptr)))
         return rc;
     SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
     if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, left->cls_dl.p, px2 * 2, hipMemcpyDeviceToHost, st));

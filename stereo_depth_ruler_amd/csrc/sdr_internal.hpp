@@ -1,6 +1,8 @@
 // sdr_internal.hpp -- launchers shared by the kernel files and sdr_engine.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "../../include/sdr/sdr.h"
 #include <stddef.h>
 #include <stdint.h>
 
@@ -51,6 +53,15 @@ struct Planes {
     int cn;
 };
 
+// MODE_SGBM_3WAY stripe-start rows (A.7): the first SH2 cost rows of stripe s > 0 with the box
+// clamped at the stripe's own start row s0, into their own buffer; computed as extra row bands
+// of the main k_cost launch (one launch per frame batch)
+constexpr int kMaxCostAux = 16;
+struct CostAux {
+    int16_t* out;  // [F][rows][W1][D], frames out_fstride apart
+    int row0, rows, s0, ylim;
+};
+
 struct CostArgs {
     Planes pl;
     int16_t* out;            // cost rows
@@ -62,6 +73,9 @@ struct CostArgs {
     int hh_bottom;           // MODE_HH: rows y>0 with y+SH2>=H keep the initial P2
     int TY;                  // tile height (output rows)
     int16_t* sink;           // cost_sink_bytes() of scratch: the stores of warm-up rows land here
+    int naux;                // stripe-start bands after the main ones (grid.y = bands + naux)
+    size_t aux_fstride;      // elements per frame of every aux buffer
+    CostAux aux[kMaxCostAux];
 };
 size_t cost_sink_bytes(const Geometry& g);
 
@@ -141,5 +155,11 @@ void launch_bgr2gray(const uint8_t* bgr, int W, int H, size_t bstride, uint8_t* 
 void launch_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* dst,
                       size_t dstride, int F, hipStream_t st);
 int selftest_wave_ops(int* failures);
+
+// DisparityWLSFilter::filter on device (sdr_wls.hip) with the class path's fused epilogue:
+// fout (nullable) = out / 16, xyz (nullable, needs fout and Q) = reprojectImageTo3D(fout, Q)
+int wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide, int W,
+                       int H, size_t gstride, size_t gfstride, int F, int16_t* out, float* conf,
+                       float* fout, const double* Q, float* xyz);
 
 }  // namespace sdr

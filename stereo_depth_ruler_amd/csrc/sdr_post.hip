@@ -374,34 +374,6 @@ void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int 
 // A.12 reprojectImageTo3D: double math, sequential sums from 0, no contraction, Vec3f then
 // *(1.0/h3) rounded to float; handleMissing: Z = 10000 where |d - min(disp)| <= FLT_EPSILON.
 // ------------------------------------------------------------------------------------------
-struct Q16 {
-    double q[16];
-};
-
-__device__ __forceinline__ void reproject_px(const Q16& Q, int x, int y, double d, double mind,
-                                             int hm, float* o) {
-#pragma clang fp contract(off)
-    const double v0 = (double)x, v1 = (double)y;
-    double h[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        double s = 0.0;
-        s += Q.q[i * 4 + 0] * v0;
-        s += Q.q[i * 4 + 1] * v1;
-        s += Q.q[i * 4 + 2] * d;
-        s += Q.q[i * 4 + 3] * 1.0;
-        h[i] = s;
-    }
-    const double ia = 1.0 / h[3];
-    const float X = (float)((double)(float)h[0] * ia);
-    const float Y = (float)((double)(float)h[1] * ia);
-    float Z = (float)((double)(float)h[2] * ia);
-    if (hm && fabs(d - mind) <= (double)FLT_EPSILON) Z = 10000.f;
-    o[0] = X;
-    o[1] = Y;
-    o[2] = Z;
-}
-
 __global__ __launch_bounds__(256) void k_reproject_s16(const int16_t* disp, int W, int H,
                                                        size_t dstride, size_t dfstride, Q16 Q,
                                                        int hm, const int* mins, float* xyz,

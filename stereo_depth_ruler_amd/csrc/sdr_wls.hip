@@ -27,6 +27,7 @@
 //                  images; k_fgs_weights builds the weights once per frame
 //   k_wls_final    FGS(conf*d) / FGS(conf) -> saturate_cast<short>, 16*(min_disp-1) outside ROI
 #include "../../include/sdr/sdr.h"
+#include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 
 #include <hip/hip_runtime.h>
@@ -262,47 +263,58 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const f
 }
 
 // FGS line solves by parallel cyclic reduction (the default solver), in the operation order of
-// oracle/wls_oracle.c fgs_line_pcr.  A 256-thread workgroup owns G lines of n samples of one
-// frame (G = 1 for long lines); equation e = g*n + k of the block lives in registers of thread
-// e mod 256 (slot e / 256), so a thread keeps its equations' (a, c, e, b, d0, d1) across the
-// log2(n) stages and only publishes what its neighbours read:
+// oracle/wls_oracle.c fgs_line_pcr.  A workgroup of T threads (blockDim.x, a multiple of 64, up
+// to 1024) owns G lines of n samples of one frame (G = 1 for long lines); equation e = g*n + k of
+// the block lives in registers of thread e mod T (slot e / T), so a thread keeps its equations'
+// (a, c, e, b, d0, d1) across the log2(n) stages and only publishes what its neighbours read:
 //   X[e] = {row sum, 1/b, d0, d1} (one 16-byte LDS word), A[e] = a, Cc[e] = c
 // Stage s reads X and A of e - s, X and Cc of e + s (zeros past the line's ends), then every
-// equation is rewritten at once; two barriers per stage.  The images are read and written in
-// place in their row-major layout: for rows (lines = rows) a block's loads are whole rows, for
-// columns (lines = columns) G adjacent columns per row; the loads and stores go through LDS with
-// consecutive threads on consecutive addresses.  Weights Cw: same layout as the images (Ch for
-// rows, Cv for columns, 0 on each line's last sample).
-constexpr int kPcrThreads = 256;
-constexpr int kPcrMaxN = 4096;  // samples per block (G * n): 16 equations per thread
+// equation is rewritten at once.  The published values are double-buffered by stage parity, so
+// a stage costs one barrier: a thread can only overwrite a buffer two stages later, after the
+// barrier every reader of it has passed.  The chip holds few lines (360 rows or 280 column pairs
+// at 640x360), so the block takes as many threads as equations (EPT = 1 up to 1024 samples):
+// several waves per SIMD hide the LDS and division latencies of the stage chain.  The images are
+// read and written in place in their row-major layout: for rows (lines = rows) a block's loads
+// are whole rows, for columns (lines = columns) G adjacent columns per row; loads and stores go
+// through LDS with consecutive threads on consecutive addresses.  Weights Cw: same layout as the
+// images (Ch for rows, Cv for columns, 0 on each line's last sample).
+constexpr int kPcrMaxN = 4096;  // samples per block (G * n): 4 equations per thread of 1024
 
 template <int EPT, bool TWO>
-__global__ __launch_bounds__(kPcrThreads) void k_fgs_pcr(float* U0, float* U1, const float* __restrict__ Cw,
-                                                         int w, int h, size_t fstride, int rows, int G,
-                                                         float lam) {
+__global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const float* __restrict__ Cw,
+                                                  int w, int h, size_t fstride, int rows, int G,
+                                                  float lam) {
     extern __shared__ float4 pcr_smem[];
+    const int T = blockDim.x;
     const int n = rows ? w : h;
     const int nlines = rows ? h : w;
     const int N = G * n;
-    float4* X = pcr_smem;               // [N] {row sum, 1/b, d0, d1}
-    float* A = (float*)(X + N);         // [N] a (sub-diagonal); the weights during the load
-    float* Cc = A + N;                  // [N] c (super-diagonal)
+    // two stage buffers: X [2][N] {row sum, 1/b, d0, d1}, then A [2][N] (a; the weights during
+    // the load), Cc [2][N] (c)
+    float4* X = pcr_smem;
+    float* A = (float*)(X + 2 * N);
+    float* Cc = A + 2 * N;
     const int tid = threadIdx.x;
-    const int l0 = blockIdx.x * G;
-    const size_t fo = (size_t)blockIdx.y * fstride;
-    // ---- coalesced load into LDS: weight -> A[e], rhs -> X[e].z/.w ----
-    for (int idx = tid; idx < N; idx += kPcrThreads) {
-        int g, k;
-        size_t off;
+    // consecutive line groups share an XCD: the column pass's G-column blocks of one row band
+    // read and write parts of the same cache lines, which then meet in one L2
+    const int gx = gridDim.x;
+    const int lb = xcd_block(blockIdx.x + gx * blockIdx.y, gx * gridDim.y);
+    const int l0 = (lb % gx) * G;
+    const size_t fo = (size_t)(lb / gx) * fstride;
+    auto addr = [&](int idx, int& g, int& k) -> size_t {
         if (rows) {
             g = idx / n;
             k = idx - g * n;
-            off = (size_t)(l0 + g) * w + k;
-        } else {
-            k = idx / G;
-            g = idx - k * G;
-            off = (size_t)k * w + l0 + g;
+            return (size_t)(l0 + g) * w + k;
         }
+        k = idx / G;
+        g = idx - k * G;
+        return (size_t)k * w + l0 + g;
+    };
+    // ---- coalesced load into LDS: weight -> A[e], rhs -> X[e].z/.w ----
+    for (int idx = tid; idx < N; idx += T) {
+        int g, k;
+        const size_t off = addr(idx, g, k);
         const int e = g * n + k;
         float cw = 0.0f, r0 = 0.0f, r1 = 0.0f;
         if (l0 + g < nlines) {
@@ -318,7 +330,7 @@ __global__ __launch_bounds__(kPcrThreads) void k_fgs_pcr(float* U0, float* U1, c
     int kk[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; j++) {
-        const int e = tid + j * kPcrThreads;
+        const int e = tid + j * T;
         kk[j] = 0;
         a[j] = c[j] = 0.0f;
         rs[j] = b[j] = 1.0f;
@@ -335,30 +347,39 @@ __global__ __launch_bounds__(kPcrThreads) void k_fgs_pcr(float* U0, float* U1, c
         }
     }
     __syncthreads();
-    for (int s = 1; s < n; s <<= 1) {
+    int buf = 0;
+    for (int s = 1; s < n; s <<= 1, buf ^= N) {
+        float4* Xb = X + buf;
+        float* Ab = A + buf;
+        float* Cb = Cc + buf;
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
-            const int e = tid + j * kPcrThreads;
+            const int e = tid + j * T;
             if (e < N) {
-                X[e] = make_float4(rs[j], 1.0f / b[j], d0[j], d1[j]);
-                A[e] = a[j];
-                Cc[e] = c[j];
+                Xb[e] = make_float4(rs[j], 1.0f / b[j], d0[j], d1[j]);
+                Ab[e] = a[j];
+                Cb[e] = c[j];
             }
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < EPT; j++) {
-            const int e = tid + j * kPcrThreads;
-            if (e < N) {
-                float4 xm = make_float4(0.0f, 0.0f, 0.0f, 0.0f), xp = xm;
-                float am = 0.0f, cp = 0.0f;
-                if (kk[j] >= s) {
-                    xm = X[e - s];
-                    am = A[e - s];
+            // branch-free: all four reads in flight at once, missing neighbours selected to zero
+            // (threads past N compute on a clamped equation and never publish)
+            const int e = min(tid + j * T, N - 1);
+            {
+                const bool hm = kk[j] >= s, hp = kk[j] + s < n;
+                const int em = hm ? e - s : e, ep = hp ? e + s : e;
+                float4 xm = Xb[em], xp = Xb[ep];
+                float am = Ab[em], cp = Cb[ep];
+                const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (!hm) {
+                    xm = z4;
+                    am = 0.0f;
                 }
-                if (kk[j] + s < n) {
-                    xp = X[e + s];
-                    cp = Cc[e + s];
+                if (!hp) {
+                    xp = z4;
+                    cp = 0.0f;
                 }
                 const float k1 = a[j] * xm.y;
                 const float k2 = c[j] * xp.y;
@@ -373,32 +394,21 @@ __global__ __launch_bounds__(kPcrThreads) void k_fgs_pcr(float* U0, float* U1, c
                 if constexpr (TWO) d1[j] = (d1[j] - xm.w * k1) - xp.w * k2;
             }
         }
-        __syncthreads();
     }
-    // ---- decoupled: u = d / b, staged in LDS for the coalesced store ----
+    // ---- decoupled: u = d / b, staged in LDS (buffer `buf`, untouched since two stages back) for
+    // the coalesced store ----
+    float4* Xo = X + buf;
 #pragma unroll
     for (int j = 0; j < EPT; j++) {
-        const int e = tid + j * kPcrThreads;
-        if (e < N) {
-            X[e].z = d0[j] / b[j];
-            if constexpr (TWO) X[e].w = d1[j] / b[j];
-        }
+        const int e = tid + j * T;
+        if (e < N) Xo[e] = make_float4(0.0f, 0.0f, d0[j] / b[j], TWO ? d1[j] / b[j] : 0.0f);
     }
     __syncthreads();
-    for (int idx = tid; idx < N; idx += kPcrThreads) {
+    for (int idx = tid; idx < N; idx += T) {
         int g, k;
-        size_t off;
-        if (rows) {
-            g = idx / n;
-            k = idx - g * n;
-            off = (size_t)(l0 + g) * w + k;
-        } else {
-            k = idx / G;
-            g = idx - k * G;
-            off = (size_t)k * w + l0 + g;
-        }
+        const size_t off = addr(idx, g, k);
         if (l0 + g >= nlines) continue;
-        const float4 x = X[g * n + k];
+        const float4 x = Xo[g * n + k];
         U0[fo + off] = x.z;
         if constexpr (TWO) U1[fo + off] = x.w;
     }
@@ -455,11 +465,129 @@ __global__ __launch_bounds__(256) void k_transpose2(const float* __restrict__ s0
     }
 }
 
+// The whole filter front end of one ROI row in one workgroup (grid: rows x frames), replacing
+// k_wls_disc + k_wls_conf + k_fgs_weights:
+//   1. vertical (2r+1)-row sums of d and d^2 of both maps over the row's window (BORDER_REFLECT_101
+//      inside the ROI), one column per thread, into LDS (int32 / int64: exact integers)
+//   2. horizontal sums of those -> the depth-discontinuity value of every ROI column of both maps
+//      (the same integers as disc_at's 2-D loop, so the same floats) into LDS
+//   3. the discontinuity-aware LR check of the row (its partner column x - (d >> 4) is in the same
+//      row, so the row's right map is all it needs): full-size confidence x255, A = conf * d,
+//      B = conf (ROI-compact)
+//   4. the row's FGS weights from the guide (Ch row-major for k_fgs_pcr or column-major for the
+//      sequential sweep, Cv row-major)
+// Rows outside the ROI only get the confidence map's 255.  Dynamic LDS: 24 B per ROI column.
+__global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl, const int16_t* __restrict__ dr,
+                                                  WlsGeom g, const uint8_t* __restrict__ guide,
+                                                  size_t gstride, size_t gfstride,
+                                                  const float* __restrict__ lut, int ch_rowmajor,
+                                                  float* __restrict__ conf_full, float* __restrict__ A,
+                                                  float* __restrict__ B, float* __restrict__ ChW,
+                                                  float* __restrict__ Cv) {
+    extern __shared__ int64_t wls_smem[];
+    const int y = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const size_t fo = (size_t)f * g.W * g.H;
+    const int i = y - g.ry;
+    if (i < 0 || i >= g.rh) {
+        if (conf_full)
+            for (int x = tid; x < g.W; x += T) conf_full[fo + (size_t)y * g.W + x] = 255.0f;
+        return;
+    }
+    const int rw = g.rw, r = g.radius;
+    int64_t* V2 = wls_smem;                // [2][rw] column sums of d^2 (left, right)
+    int* V = (int*)(V2 + 2 * rw);          // [2][rw] column sums of d
+    float* disc = (float*)(V + 2 * rw);    // [2][rw] discontinuity values
+    const int16_t* L = dl + fo;
+    const int16_t* R = dr + fo;
+    for (int j = tid; j < rw; j += T) {
+        int s0 = 0, s1 = 0;
+        int64_t q0 = 0, q1 = 0;
+        for (int a = -r; a <= r; a++) {
+            const size_t ro = (size_t)(g.ry + reflect101(i + a, g.rh)) * g.W;
+            const int vl = L[ro + g.rx + j], vr = R[ro + g.rrx + j];
+            s0 += vl;
+            q0 += (int64_t)vl * vl;
+            s1 += vr;
+            q1 += (int64_t)vr * vr;
+        }
+        V[j] = s0;
+        V[rw + j] = s1;
+        V2[j] = q0;
+        V2[rw + j] = q1;
+    }
+    __syncthreads();
+    for (int j = tid; j < rw; j += T) {
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            long long s = 0, s2 = 0;
+            for (int b = -r; b <= r; b++) {
+                const int jj = reflect101(j + b, rw);
+                s += V[m * rw + jj];
+                s2 += V2[m * rw + jj];
+            }
+            const float mean = (float)((double)s * g.scale);
+            const float msq = (float)((double)s2 * g.scale);
+            const float var = msq - mean * mean;
+            const float c = 1.0f - g.roll_off * var;
+            disc[m * rw + j] = c > 0.0f ? c : 0.0f;
+        }
+    }
+    __syncthreads();
+    const size_t cf = (size_t)f * rw * g.rh + (size_t)i * rw;
+    for (int x = tid; x < g.W; x += T) {
+        const size_t o = (size_t)y * g.W + x;
+        const int j = x - g.rx;
+        const bool in_roi = j >= 0 && j < rw;
+        float c = 1.0f;
+        int v = 0;
+        if (in_roi) {
+            c = disc[j];
+            v = L[o];
+            const int ridx = x - (v >> 4);
+            if (ridx >= g.rrx && ridx < g.rrx + rw) {
+                if (abs(v + (int)R[(size_t)y * g.W + ridx]) < g.lrc_thresh) {
+                    const float rc = disc[rw + ridx - g.rrx];
+                    c = c < rc ? c : rc;
+                } else {
+                    c = 0.0f;
+                }
+            }
+        }
+        const float conf = 255.0f * c;
+        if (conf_full) conf_full[fo + o] = conf;
+        if (in_roi) {
+            A[cf + j] = conf * (float)v;
+            B[cf + j] = conf;
+        }
+    }
+    // FGS weights of the guide's ROI row i (k_fgs_weights' formulas)
+    const uint8_t* gr = guide + (size_t)f * gfstride + (size_t)(g.ry + i) * gstride + g.rx;
+    const size_t wfo = (size_t)f * rw * g.rh;
+    for (int j = tid; j < rw; j += T) {
+        const int v = gr[j];
+        float ch = 0.0f, cv = 0.0f;
+        if (j + 1 < rw) {
+            const int d = v - gr[j + 1];
+            ch = lut[d * d];
+        }
+        if (i + 1 < g.rh) {
+            const int d = v - gr[gstride + j];
+            cv = lut[d * d];
+        }
+        ChW[wfo + (ch_rowmajor ? (size_t)i * rw + j : (size_t)j * g.rh + i)] = ch;
+        Cv[wfo + (size_t)i * rw + j] = cv;
+    }
+}
+
 // saturate_cast<short>(float): round half to even, saturate; 0 where FGS(conf) == 0 (cv::divide
 // of floats returns 0 for a zero divisor)
+// Optional epilogue of the class path (stereo_disparity.cpp:34, :76-80), fused: fout = out / 16
+// (convertTo(CV_32F, 1/16)) and xyz = reprojectImageTo3D(fout, Q) (computeDepth,
+// handleMissing = false).
 __global__ __launch_bounds__(256) void k_wls_final(const float* __restrict__ A,
                                                    const float* __restrict__ B, WlsGeom g,
-                                                   int16_t* __restrict__ out) {
+                                                   int16_t* __restrict__ out, float* __restrict__ fout,
+                                                   Q16 Q, float* __restrict__ xyz) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= g.W || y >= g.H) return;
@@ -476,6 +604,11 @@ __global__ __launch_bounds__(256) void k_wls_final(const float* __restrict__ A,
         r = fabsf(v) < 2147483648.0f ? (int16_t)(int)q : (int16_t)-32768;
     }
     out[o] = r;
+    if (fout) {
+        const float df = (float)r * 0.0625f;
+        fout[o] = df;
+        if (xyz) reproject_px(Q, x, y, (double)df, 0.0, 0, xyz + 3 * o);
+    }
 }
 
 // FastGlobalSmootherFilter::filter on nimg (1 or 2) row-major w x h images per frame (R0, R1, in
@@ -491,27 +624,25 @@ static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const flo
     else hipLaunchKernelGGL((k_fgs_sweep<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
 }
 
-// k_fgs_pcr instance for G*n samples per block (EPT equations per thread)
+// k_fgs_pcr instance for G*n samples per block: one equation per thread up to 1024 samples
+// (T = the samples rounded up to whole waves), 2 or 4 per thread of 1024 beyond
 template <bool TWO>
 static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F, int rows,
                       float lam, hipStream_t st) {
     const int n = rows ? w : h, nlines = rows ? h : w;
     if (n > kPcrMaxN) return -1;
-    // short lines: G per block so that a block holds up to 768 samples (3 per thread)
-    const int G = std::max(1, std::min(nlines, 768 / n));
+    // short lines: G per block so that a block holds up to 1024 samples
+    const int G = std::max(1, std::min(nlines, 1024 / n));
     const int N = G * n;
-    const int need = (N + kPcrThreads - 1) / kPcrThreads;
-    const dim3 grid((nlines + G - 1) / G, F), blk(kPcrThreads);
-    const size_t lds = (size_t)N * 24;
+    const int ept = N <= 1024 ? 1 : N <= 2048 ? 2 : 4;
+    const int T = std::min(1024, ((N + ept - 1) / ept + 63) / 64 * 64);
+    const dim3 grid((nlines + G - 1) / G, F), blk(T);
+    const size_t lds = (size_t)N * 48;
     const size_t fs = (size_t)w * h;
-#define SDR_PCR(E)                                                                                     \
-    if (need <= E) {                                                                                   \
-        hipLaunchKernelGGL((k_fgs_pcr<E, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam); \
-        return 0;                                                                                      \
-    }
-    SDR_PCR(1) SDR_PCR(2) SDR_PCR(3) SDR_PCR(4) SDR_PCR(6) SDR_PCR(8) SDR_PCR(12) SDR_PCR(16)
-#undef SDR_PCR
-    return -1;
+    if (ept == 1) hipLaunchKernelGGL((k_fgs_pcr<1, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
+    else if (ept == 2) hipLaunchKernelGGL((k_fgs_pcr<2, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
+    else hipLaunchKernelGGL((k_fgs_pcr<4, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
+    return 0;
 }
 
 // FastGlobalSmootherFilter::filter on R0 (and R1 when non-null: a second right-hand side of the
@@ -523,11 +654,13 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
 // Scratch (each F*w*h floats): A, B (column-major copies, THOMAS), T (THOMAS), ChT, Cv (weights).
 static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
-                      int iters, int solver, const FgsScratch& s, hipStream_t st) {
+                      int iters, int solver, const FgsScratch& s, hipStream_t st,
+                      bool weights_ready = false) {
     const size_t fs = (size_t)w * h;
     const bool pcr = solver == SDR_FGS_PCR;
-    hipLaunchKernelGGL(k_fgs_weights, dim3((w + 63) / 64, (h + 3) / 4, F), dim3(256), 0, st, guide,
-                       gstride, gfstride, lut, w, h, pcr ? 1 : 0, s.ChT, s.Cv);
+    if (!weights_ready)
+        hipLaunchKernelGGL(k_fgs_weights, dim3((w + 63) / 64, (h + 3) / 4, F), dim3(256), 0, st, guide,
+                           gstride, gfstride, lut, w, h, pcr ? 1 : 0, s.ChT, s.Cv);
     const dim3 t_rm((w + 63) / 64, (h + 63) / 64, F), t_cm((h + 63) / 64, (w + 63) / 64, F);
     float lam = (float)lambda;
     const float fa = (float)att;
@@ -699,12 +832,20 @@ int sdr_wls_get_roi(const sdr_wls* h, int W, int H, int roi[4]) {
     return SDR_OK;
 }
 
-int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide,
-                          int W, int H, size_t gstride, size_t gfstride, int F, int16_t* out,
-                          float* conf) {
+}  // extern "C"
+
+// DisparityWLSFilter::filter on device with the class path's optional fused epilogue (fout =
+// out / 16, xyz = reprojectImageTo3D(fout, Q)); sdr_wls_filter_device is this with neither.
+// ROIs up to kPcrMaxN columns take the fused front end (k_wls_prep: discontinuity maps, LR check,
+// confidence, FGS weights in one launch); wider ones the per-pixel k_wls_disc / k_wls_conf /
+// k_fgs_weights kernels.
+int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide,
+                            int W, int H, size_t gstride, size_t gfstride, int F, int16_t* out,
+                            float* conf, float* fout, const double* Q, float* xyz) {
     if (!h || !dl || !dr || !guide || !out) return sdr::set_error(SDR_ERR_ARG, "null argument");
     if (W <= 0 || H <= 0 || F <= 0 || gstride < (size_t)W || (F > 1 && gfstride < gstride * H))
         return sdr::set_error(SDR_ERR_ARG, "bad size/stride");
+    if (xyz && (!fout || !Q)) return sdr::set_error(SDR_ERR_ARG, "the fused reprojection needs fout and Q");
     WLS_HIP(hipSetDevice(h->device));
     hipStream_t st = h->stream;
     const sdr_wls_params& p = h->p;
@@ -727,35 +868,57 @@ int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, cons
     if (roi && p.fgs_solver == SDR_FGS_PCR && (g.rw > sdr::kPcrMaxN || g.rh > sdr::kPcrMaxN))
         return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                             "(use SDR_FGS_THOMAS for larger ROIs)");
+    const bool fused = roi && g.rw <= sdr::kPcrMaxN;
     const size_t cpx = roi ? (size_t)g.rw * g.rh : 0;
     int rc;
     const float* lut = nullptr;
-    if ((rc = sdr::ensure(h->rdisc, F * px * 4))) return rc;
-    for (sdr::Buf* b : {&h->A, &h->B, &h->Ac, &h->Bc, &h->T, &h->ChT, &h->Cv})
+    if (!fused && (rc = sdr::ensure(h->rdisc, F * px * 4))) return rc;
+    for (sdr::Buf* b : {&h->A, &h->B, &h->ChT, &h->Cv})
         if ((rc = sdr::ensure(*b, F * cpx * 4 + 4))) return rc;
+    if (p.fgs_solver == SDR_FGS_THOMAS)
+        for (sdr::Buf* b : {&h->Ac, &h->Bc, &h->T})
+            if ((rc = sdr::ensure(*b, F * cpx * 4 + 4))) return rc;
     if ((rc = upload_lut(h, p.sigma_color, &lut))) return rc;
     float* A = (float*)h->A.p;
     float* B = (float*)h->B.p;
     const dim3 blk(256);
-    if (roi) {
-        hipLaunchKernelGGL(sdr::k_wls_disc, dim3((g.rw + 63) / 64, (g.rh + 3) / 4, F), blk, 0, st,
-                           dr, g, (float*)h->rdisc.p);
-    }
+    const bool rowmajor = p.fgs_solver == SDR_FGS_PCR;
     const dim3 grid((W + 63) / 64, (H + 3) / 4, F);
-    hipLaunchKernelGGL(sdr::k_wls_conf, grid, blk, 0, st, dl, dr, (const float*)h->rdisc.p, g,
-                       conf, A, B);
+    if (fused) {
+        hipLaunchKernelGGL(sdr::k_wls_prep, dim3(H, F), blk, (size_t)g.rw * 24, st, dl, dr, g, guide,
+                           gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
+                           (float*)h->Cv.p);
+    } else {
+        if (roi)
+            hipLaunchKernelGGL(sdr::k_wls_disc, dim3((g.rw + 63) / 64, (g.rh + 3) / 4, F), blk, 0, st,
+                               dr, g, (float*)h->rdisc.p);
+        hipLaunchKernelGGL(sdr::k_wls_conf, grid, blk, 0, st, dl, dr, (const float*)h->rdisc.p, g,
+                           conf, A, B);
+    }
     if (roi) {
         const uint8_t* g0 = guide + (size_t)g.ry * gstride + g.rx;
         const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
                                  (float*)h->Cv.p};
         if (sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
-                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st))
+                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused))
             return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                                 "(use SDR_FGS_THOMAS for larger ROIs)");
     }
-    hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out);
+    sdr::Q16 q{};
+    if (Q)
+        for (int t = 0; t < 16; t++) q.q[t] = Q[t];
+    hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out, fout, q, xyz);
     WLS_HIP(hipGetLastError());
     return SDR_OK;
+}
+
+extern "C" {
+
+int sdr_wls_filter_device(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide,
+                          int W, int H, size_t gstride, size_t gfstride, int F, int16_t* out,
+                          float* conf) {
+    return sdr::wls_filter_enqueue(h, dl, dr, guide, W, H, gstride, gfstride, F, out, conf, nullptr,
+                                   nullptr, nullptr);
 }
 
 int sdr_wls_filter(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide, int W,

@@ -72,13 +72,13 @@ class LiveLoop:
                                        self.batch, self.left_rect.data_ptr() if disp_on else None, None,
                                        self.small_l.data_ptr(), self.small_r.data_ptr()))
         check(L.sdr_sgbm_set_stream(self.left._h, s))
-        check(L.sdr_stereo_class_compute_device(self.left._h, self.right._h, self.wls._h,
-                                                self.small_l.data_ptr(), self.small_r.data_ptr(),
-                                                self.w2, self.h2, self.batch, self.disp.data_ptr(),
-                                                self.filtered.data_ptr(), None))
-        # computeDepth: reprojectImageTo3D(half-res disparity, full-res Q) (stereo_disparity.cpp:76-80)
-        check(L.sdr_reproject_device(self.disp.data_ptr(), self.w2, self.h2, self.w2, _Q(self.Q), 0,
-                                     self.depth.data_ptr(), self.w2 * 3, self.batch, s))
+        # computeDisparity + computeDepth: reprojectImageTo3D(half-res disparity, full-res Q)
+        # (stereo_disparity.cpp:76-80), fused into the WLS filter's epilogue
+        check(L.sdr_stereo_class_depth_device(self.left._h, self.right._h, self.wls._h,
+                                              self.small_l.data_ptr(), self.small_r.data_ptr(),
+                                              self.w2, self.h2, self.batch, self.disp.data_ptr(),
+                                              self.filtered.data_ptr(), None, _Q(self.Q),
+                                              self.depth.data_ptr()))
         if disp_on:  # stereo_displayer.cpp:164-173
             d, F, w2, h2 = self.display, self.batch, self.w2, self.h2
             check(L.sdr_display_set_stream(d._h, s))

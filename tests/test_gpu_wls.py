@@ -205,3 +205,24 @@ def test_create_wls_mutates_matcher():
     f.setSigmaColor(1.1)
     assert f.getLambda() == 8000.0 and abs(f.getSigmaColor() - 1.1) < 1e-12
     assert f.getDepthDiscontinuityRadius() == 3 and f.getROI(640, 360) == (80, 0, 560, 360)
+
+
+def test_wls_wide_roi_fallback(oracle):
+    """A ROI wider than k_wls_prep / k_fgs_pcr take (4096 columns): the per-pixel front end and the
+    sequential solver, still bit-exact; the default PCR solver refuses it with SDR_ERR_SIZE."""
+    rng = np.random.default_rng(4)
+    h, w = 6, 4200
+    base = rng.integers(2, 40, (h, w // 8 + 1)) * 16
+    dl = np.repeat(base, 8, 1)[:, :w].astype(np.int16)
+    dr = -np.roll(dl, -2, 1)
+    g = rng.integers(0, 256, (h, w)).astype(np.uint8)
+    q = oracle.wls_params_for_sgbm(0, 32, 5, w, h, 8000.0, 1.1)
+    f = make_filter(q, w, h)
+    with pytest.raises(sdr.SDRError):
+        f.filter(dl, g, dr)
+    q.fgs_solver = FGS_THOMAS
+    f.setFgsSolver(FGS_THOMAS)
+    ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)
+    got = f.filter(dl, g, dr)
+    assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf))
+    assert np.array_equal(got, ref)

@@ -190,6 +190,12 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses the N>1 path with every "
                          "rank on the one GPU of a 1-GPU box (gather staged through host memory)")
+    ap.add_argument("--status-every", type=int, default=16,
+                    help="N>1: ranks exchange their step status (host-side, gloo) every this many steps "
+                         "and after the last; a failed rank keeps joining the gathers with zeros until "
+                         "then, and every rank exits non-zero (RankFailure) instead of blocking")
+    ap.add_argument("--inject-failure", default=None, metavar="RANK:STEP",
+                    help="test hook: rank RANK's step STEP raises SDR_ERR_ARG (failure-path tests)")
     a = ap.parse_args()
 
     import torch
@@ -199,15 +205,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gloo = a.dist_backend == "gloo"
+    from stereo_depth_ruler_amd.distributed import check_ranks, error_code, init_process_group
+
     if world > 1:
+        # every collective bounded by SDR_DIST_TIMEOUT (default 120 s): a rank that dies outright
+        # cannot leave the others blocked (stereo_depth_ruler_amd/distributed.py)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if gloo:
             local = local % torch.cuda.device_count()
             torch.cuda.set_device(local)
-            dist.init_process_group("gloo")
+            init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -273,6 +283,9 @@ def main():
                        for _ in range(2 * ns)]
     pending = [None] * (2 * ns)
     sent = {}  # slot -> the tensor this rank handed to that slot's last gather
+    failure = {"code": 0, "err": None}  # this rank's first failed step (reported at the next check)
+    inject = tuple(int(v) for v in a.inject_failure.split(":")) if a.inject_failure else None
+    from stereo_depth_ruler_amd._lib import SDRError
 
     def step(i):
         j = (i * batch) % (nf - batch + 1) if nf > batch else 0
@@ -284,7 +297,19 @@ def main():
             if pending[slot] is not None:
                 pending[slot].wait()
                 pending[slot] = None
-            res = run(j, k, slot)
+            try:
+                if inject is not None and inject == (rank, i):
+                    raise SDRError(-1, f"injected failure at rank {rank} step {i}")
+                res = run(j, k, slot)
+            except Exception as e:  # noqa: BLE001 -- any failed step is reported to every rank
+                if world == 1:
+                    raise
+                if failure["err"] is None:
+                    failure["code"], failure["err"] = error_code(e), e
+                    log(f"rank {rank}: step {i} failed ({e!r}); reporting at the next status check")
+                res = torch.zeros((gather_bytes,), dtype=torch.uint8, device=dev)
+            if world > 1 and ((i + 1) % max(1, a.status_every) == 0):
+                check_ranks(failure["code"])  # RankFailure on every rank if any step failed
             if world > 1:
                 # gather this step's disparity from every rank; a later step reuses the slot only
                 # after this collective has completed
@@ -301,6 +326,8 @@ def main():
     for p in pending:
         if p is not None:
             p.wait()
+    if world > 1:
+        check_ranks(failure["code"])
     pending = [None] * (2 * ns)
     torch.cuda.synchronize()
     if not a.no_kernel_timing and a.in_flight_timing:
@@ -317,6 +344,7 @@ def main():
             p.wait()
     torch.cuda.synchronize()
     if world > 1:
+        check_ranks(failure["code"])
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0

@@ -476,7 +476,8 @@ __global__ __launch_bounds__(256) void k_transpose2(const float* __restrict__ s0
 //      B = conf (ROI-compact)
 //   4. the row's FGS weights from the guide (Ch row-major for k_fgs_pcr or column-major for the
 //      sequential sweep, Cv row-major)
-// Rows outside the ROI only get the confidence map's 255.  Dynamic LDS: 24 B per ROI column.
+// Rows outside the ROI only get the confidence map's 255.  Dynamic LDS: 32 B per ROI column
+// (int64 + int32 column sums and a float discontinuity value, per map).
 __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl, const int16_t* __restrict__ dr,
                                                   WlsGeom g, const uint8_t* __restrict__ guide,
                                                   size_t gstride, size_t gfstride,
@@ -885,7 +886,7 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     const bool rowmajor = p.fgs_solver == SDR_FGS_PCR;
     const dim3 grid((W + 63) / 64, (H + 3) / 4, F);
     if (fused) {
-        hipLaunchKernelGGL(sdr::k_wls_prep, dim3(H, F), blk, (size_t)g.rw * 24, st, dl, dr, g, guide,
+        hipLaunchKernelGGL(sdr::k_wls_prep, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
                            gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
                            (float*)h->Cv.p);
     } else {

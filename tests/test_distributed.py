@@ -9,7 +9,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from stereo_depth_ruler_amd.distributed import frames_per_rank, gather_frames, shard_frames
+from stereo_depth_ruler_amd.distributed import (RankFailure, check_ranks, frames_per_rank, gather_frames,
+                                                shard_frames)
 
 
 def test_shard_round_robin_covers_all():
@@ -34,9 +35,11 @@ def _worker(rank, world, port, n_frames, q):
     from oracle import oracle as O
     from stereo_depth_ruler_amd import synthetic as S
 
+    from stereo_depth_ruler_amd.distributed import init_process_group
+
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_process_group("gloo", rank=rank, world_size=world)
     p = O.make_params(0, 16, 5, 600, 2400, 1, 63, 12, 20, 2, 0)
     mine = shard_frames(n_frames, world, rank)
     res = []
@@ -70,3 +73,75 @@ def test_gloo_world2_gather_matches_single(n_frames):
     for i in range(n_frames):
         L, R, _ = S.make_pair(24, 64, 16, seed=i)
         assert np.array_equal(got[i], O.sgbm_compute(L, R, p)), i
+
+
+def _failing_worker(rank, world, port, fail_rank, q):
+    """Rank `fail_rank` fails its step with an engine-style error; every rank must raise
+    RankFailure from gather_frames (none may block in the gather) and exit non-zero."""
+    import sys
+    import time
+
+    import torch.distributed as dist
+
+    from stereo_depth_ruler_amd._lib import SDRError
+    from stereo_depth_ruler_amd.distributed import init_process_group
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    init_process_group("gloo", rank=rank, world_size=world, timeout=30)
+    local, err = torch.zeros((2, 8, 8), dtype=torch.int16), None
+    if rank == fail_rank:
+        err = SDRError(-2, "numDisparities must be positive and divisible by 16")
+        local = None
+    t0 = time.time()
+    try:
+        gather_frames(local, 4, world, rank, error=err)
+    except RankFailure as f:
+        q.put((rank, f.codes, time.time() - t0))
+        dist.destroy_process_group()
+        sys.exit(3)
+    q.put((rank, None, time.time() - t0))
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_gloo_world2_rank_failure_aborts_gather(fail_rank):
+    """SURVEY.md 5 failure detection: one rank's SDR_ERR_* makes BOTH processes exit non-zero
+    quickly (well inside the collective timeout), with the failing rank's code reported."""
+    import time
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    t0 = time.time()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(timeout=90)
+    alive = [pr for pr in procs if pr.is_alive()]
+    for pr in alive:
+        pr.kill()
+    assert not alive, "a rank hung"
+    assert all(pr.exitcode == 3 for pr in procs), [pr.exitcode for pr in procs]
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    for rank, codes, dt in res:
+        assert codes is not None and codes[fail_rank] == -2 and codes[1 - fail_rank] == 0
+        assert dt < 20
+    assert time.time() - t0 < 90
+
+
+def test_check_ranks_single_process():
+    """world 1: the status exchange is a no-op on success and raises on failure."""
+    import torch.distributed as dist
+
+    from stereo_depth_ruler_amd.distributed import init_process_group
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    init_process_group("gloo", rank=0, world_size=1, timeout=30)
+    try:
+        check_ranks(0)
+        with pytest.raises(RankFailure):
+            check_ranks(-4)
+    finally:
+        dist.destroy_process_group()

@@ -4,7 +4,9 @@ spawned processes (gloo, both ranks on cuda:0) each run the engine on their fram
   - gather_frames: rank 0's gathered disparities equal a single-process run of all frames on the
     same engine, bit for bit (and the oracle on two of them);
   - bench.py's own step/async-gather loop under torch.distributed.run (--dist-backend gloo): the
-    JSON line reports 2 ranks and its end-to-end gather check passes.
+    JSON line reports 2 ranks and its end-to-end gather check passes;
+  - the failure path: a rank whose engine call returns SDR_ERR_* makes BOTH processes
+    exit non-zero promptly (gather_frames and bench.py), no rank blocks in a collective.
 
 Scaling is not measured here (both ranks share one GPU); the RCCL path is the same code with
 backend "nccl" and one GPU per rank.
@@ -53,9 +55,9 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
 
     import stereo_depth_ruler_amd as sdr
-    from stereo_depth_ruler_amd.distributed import gather_frames, shard_frames
+    from stereo_depth_ruler_amd.distributed import gather_frames, init_process_group, shard_frames
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     Ls, Rs = _frames()
     mine = shard_frames(N, world, rank)
@@ -109,3 +111,74 @@ def test_world2_bench_step_gather_loop():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["steps"] == 6
     assert out["gather_check"] == {"step": 7, "ranks": 2, "ok": True}
+
+
+def _failing_worker(rank, world, port, q):
+    """Rank 1 asks the real engine for numDisparities = 20 (SDR_ERR_NUMDISP, OpenCV's assert)."""
+    import sys
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import stereo_depth_ruler_amd as sdr
+    from stereo_depth_ruler_amd.distributed import RankFailure, gather_frames, init_process_group, shard_frames
+
+    init_process_group("gloo", rank=rank, world_size=world, timeout=60)
+    torch.cuda.set_device(0)
+    Ls, Rs = _frames()
+    mine = shard_frames(N, world, rank)
+    args = ARGS if rank == 0 else (0, 20) + ARGS[2:]
+    local, err = None, None
+    t0 = time.time()
+    try:
+        m = sdr.StereoSGBM.create(*args)
+        local = m.compute(torch.from_numpy(Ls[mine]).cuda(), torch.from_numpy(Rs[mine]).cuda()).cpu()
+    except sdr.SDRError as e:
+        err = e
+    try:
+        gather_frames(local, N, world, rank, error=err)
+    except RankFailure as f:
+        q.put((rank, f.codes, time.time() - t0))
+        dist.destroy_process_group()
+        sys.exit(3)
+    q.put((rank, None, time.time() - t0))
+
+
+def test_world2_engine_error_aborts_gather():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a rank hung"
+    assert [p.exitcode for p in procs] == [3, 3]
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    for rank, codes, dt in res:
+        assert codes == [0, -2], codes  # SDR_ERR_NUMDISP on rank 1
+        assert dt < 60
+
+
+def test_world2_bench_rank_failure_exits_nonzero():
+    """bench.py with rank 1's step 5 failing: both ranks raise RankFailure at the next status
+    check (every 4 steps here) and torch.distributed.run exits non-zero, well inside the timeout."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1", SDR_DIST_TIMEOUT="60")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "8", "--warmup", "2", "--dist-backend", "gloo", "--streams", "2",
+           "--frames", "4", "--no-cpu-baseline", "--no-kernel-timing", "--status-every", "4",
+           "--inject-failure", "1:5"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode != 0
+    assert "RankFailure" in res.stderr and "injected failure at rank 1 step 5" in res.stderr, res.stderr[-3000:]
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]

@@ -46,11 +46,13 @@ void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st) {
 __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ Limg,
                                                    const uint8_t* __restrict__ Rimg, size_t stride,
                                                    size_t fstride, int W, int H, int ftzero,
-                                                   Planes pl) {
+                                                   Planes pl, int split) {
     extern __shared__ uint64_t q6[];  // [W] 6 bytes per pixel, then the 3 input rows [3][W*cn] bytes
     const int y = blockIdx.x, img = blockIdx.y, f = blockIdx.z;
     const int cn = pl.cn, WB = W * cn;
-    const uint8_t* base = (img ? Rimg : Limg) + (size_t)f * fstride;
+    // paired matchers: frame f >= split is frame f - split of the pair with L and R swapped
+    const bool swap = f >= split;
+    const uint8_t* base = ((img != 0) != swap ? Rimg : Limg) + (size_t)(swap ? f - split : f) * fstride;
     {
         // the row and its neighbours (replicated at the borders) staged in LDS: one coalesced
         // byte load per pixel and row instead of eleven scattered ones
@@ -128,9 +130,9 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
 }
 
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
-                      int H, int F, int ftzero, const Planes& pl, hipStream_t st) {
+                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split) {
     hipLaunchKernelGGL(k_prefilter, dim3(H, 2, F), dim3(256), (size_t)W * (8 + 3 * pl.cn), st, L, R,
-                       stride, fstride, W, H, ftzero, pl);
+                       stride, fstride, W, H, ftzero, pl, split);
 }
 
 }  // namespace sdr

@@ -337,8 +337,9 @@ __global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
     }
     if (ty0 >= ty1) return;
     const int bx0 = bx * Cfg::BCOLS;
-    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, CN, true>(g, aa, lds, bx, f, ty0, ty1);
-    else cost_block<NR, K, CN, false>(g, aa, lds, bx, f, ty0, ty1);
+    const Geometry gf = frame_geom(g, f);
+    if (bx0 - Cfg::SW2 < 0 || bx0 + Cfg::BCOLS + Cfg::SW2 > g.W1) cost_block<NR, K, CN, true>(gf, aa, lds, bx, f, ty0, ty1);
+    else cost_block<NR, K, CN, false>(gf, aa, lds, bx, f, ty0, ty1);
 }
 
 template <int NR, int K, int CN>

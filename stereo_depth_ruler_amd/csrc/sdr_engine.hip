@@ -59,6 +59,9 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     int maxD = g.minD + g.D;
     g.minX1 = std::max(maxD, 0);
     g.W1 = W + std::min(g.minD, 0) - g.minX1;
+    g.split = 1 << 30;  // unpaired (see sdr::Geometry)
+    g.minDb = g.minD;
+    g.minX1b = g.minX1;
     if (p.mode == SDR_MODE_SGBM_3WAY) {
         g.SW2 = g.SH2 = p.blockSize > 0 ? p.blockSize / 2 : 1;
     } else {
@@ -319,7 +322,7 @@ struct sdr_sgbm {
     hipStream_t own_stream = nullptr;
     Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hxyz, keys2;
     HostXfer hx;  // pinned staging of the host-pointer entry points
-    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_dr, cls_wls, cls_f, cls_conf, cls_filt;
+    Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // per-kernel event pairs (timing level 2), harvested by sdr_sgbm_kernel_time
@@ -334,6 +337,11 @@ struct sdr_sgbm {
     // the new stream wait for it, so one matcher used from two streams never overlaps itself
     hipEvent_t done = nullptr;
     bool pending = false;
+    // the last compute skipped the no-op LR check (disp12MaxDiff >= D): debug stage 2 is then
+    // rebuilt on request from the WTA map with this geometry
+    bool lr_skipped = false;
+    sdr::Geometry lr_g{};
+    int lr_frames = 0;
 };
 
 namespace {
@@ -402,13 +410,33 @@ static int npaths_of(int mode) {
 // C read + the other L reads) = 6P - 2 bytes, 4 fewer than the canonical 2 + 6P of SURVEY.md 8(d).
 //   out (nullable): dense [F][H][W] int16 destination for the final map (else internal buffer)
 //   out_min (nullable): per-frame minimum of the final map (reprojectImageTo3D handleMissing)
+// Paired matchers (the class path): frames [0, F/2) run h's parameters on (L, R), frames
+// [F/2, F) the right matcher's `pair` parameters on (R, L) -- right_matcher->compute(R, L) -- in
+// the same launches.  Only when the two differ in minDisparity alone and match the same number
+// of columns (createRightMatcher + the WLS filter's mutations give exactly that).
+static bool can_pair(const Eff& a, const Eff& b) {
+    return a.g.W1 == b.g.W1 && a.g.W1 > 0 && a.g.D == b.g.D && a.g.SW2 == b.g.SW2 && a.g.P1 == b.g.P1 &&
+           a.g.P2 == b.g.P2 && a.mode == b.mode && a.uniq == b.uniq && a.uniq_simd == b.uniq_simd &&
+           a.disp12MaxDiff == b.disp12MaxDiff && a.ftzero == b.ftzero && a.nstripes == b.nstripes &&
+           a.speckle_ws == 0 && b.speckle_ws == 0 && a.blockSize == b.blockSize;
+}
+
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
-                           int16_t** final_disp, int cn = 1) {
+                           int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr) {
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
     if ((rc = check_channels(e, cn))) return rc;
+    if (pair) {
+        Eff eb;
+        if ((rc = make_eff(*pair, W, H, &eb))) return rc;
+        if (!can_pair(e, eb) || (F & 1)) return fail(SDR_ERR_ARG, "matchers cannot be paired");
+        e.g.split = F / 2;
+        e.g.minDb = eb.g.minD;
+        e.g.minX1b = eb.g.minX1;
+    }
+    h->lr_skipped = false;
     const sdr::Geometry& g = e.g;
     hipStream_t st = h->stream;
     const size_t px = (size_t)W * H;
@@ -464,7 +492,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     pl.R = (uint64_t*)h->planesR.p;
     pl.fstrideL = pl.fstrideR = 3 * px * cn;
     pl.cn = cn;
-    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st); }
+    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st, g.split); }
 
     sdr::CostArgs ca{};
     ca.pl = pl;
@@ -565,15 +593,29 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     wa.uniq = e.uniq;
     wa.uniq_simd = e.uniq_simd;
     { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
-    { KTimer kt(h, SDR_KERNEL_LR_CHECK); sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st); }
     const bool speckle = e.speckle_ws > 0;
+    // A.9 can only invalidate a pixel when |disp2 - d| > disp12MaxDiff; both lie in [minD, maxD),
+    // so from disp12MaxDiff >= D on (ximgproc's WLS filter sets 1000000 on the class path's left
+    // matcher, createRightMatcher on the right one) the check is the identity on the matched
+    // columns and INVALID elsewhere: the median reads the WTA map with that column mask instead
+    h->lr_skipped = !speckle && e.disp12MaxDiff >= g.D;
+    h->lr_g = g;
+    h->lr_frames = F;
+    if (!h->lr_skipped) {
+        KTimer kt(h, SDR_KERNEL_LR_CHECK);
+        sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st);
+    }
     if (speckle) {
         // the median filter runs inside the labelling's first pass (dfin = median of dlr)
         KTimer kt(h, SDR_KERNEL_SPECKLE);
         sdr::launch_speckle(dfin, dst, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
                             (int*)h->labels.p, (int*)h->sizes.p, out_min, st, dlr, dfin);
     } else {
-        { KTimer kt(h, SDR_KERNEL_MEDIAN); sdr::launch_median3(dlr, dst, W, H, F, st); }
+        {
+            KTimer kt(h, SDR_KERNEL_MEDIAN);
+            if (h->lr_skipped) sdr::launch_median3_cols(draw, dst, g, F, st);
+            else sdr::launch_median3(dlr, dst, W, H, F, st);
+        }
         if (out_min) {
             KTimer kt(h, SDR_KERNEL_REPROJECT);
             sdr::launch_min_s16(dst, px, px, F, out_min, st);
@@ -648,7 +690,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (Buf* b : {&h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hxyz, &h->cls_bgr,
-                   &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_dr, &h->cls_wls, &h->cls_f,
+                   &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})
         if (b->p) (void)hipFree(b->p);
     h->hx.release();
@@ -1012,18 +1054,29 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
     hipStream_t st = left->stream;
     const size_t px2 = (size_t)w2 * h2;
     int rc;
-    if ((rc = ensure(left->cls_dl, F * px2 * 2))) return rc;
-    if ((rc = ensure(left->cls_dr, F * px2 * 2))) return rc;
+    // dl and dr are one buffer [2F][h][w]: the paired launch writes both
+    if ((rc = ensure(left->cls_dl, 2 * F * px2 * 2))) return rc;
     if ((rc = ensure(left->cls_wls, d_filtered ? 0 : F * px2 * 2))) return rc;
     int16_t* dl = (int16_t*)left->cls_dl.p;
-    int16_t* dr = (int16_t*)left->cls_dr.p;
+    int16_t* dr = dl + F * px2;
     int16_t* dw = d_filtered ? d_filtered : (int16_t*)left->cls_wls.p;
-    // right_matcher->compute(R, L) (stereo_disparity.cpp:28) and matcher->compute(L, R) (:27) are
-    // independent until the WLS filter: the right one runs on a side stream forked from the
-    // caller's and joined back before the filter (at 640x360 each matcher's row chains fill
-    // under a third of the chip, so the two overlap)
+    // matcher->compute(L, R) (stereo_disparity.cpp:27) and right_matcher->compute(R, L) (:28) are
+    // independent until the WLS filter.  When the right matcher differs from the left one in
+    // minDisparity alone (createRightMatcher after createDisparityWLSFilter: always on the class
+    // path) both run as ONE batch of 2F frames through the same launches: at 640x360 a matcher's
+    // row chains fill under a third of the chip, and no stream fork/join is needed.  Otherwise
+    // the right one runs on a side stream forked from the caller's and joined back before the filter.
     int16_t* fin = nullptr;
+    bool paired = false;
     if (right) {
+        Eff el, er;
+        paired = make_eff(left->p, w2, h2, &el) == SDR_OK && make_eff(right->p, w2, h2, &er) == SDR_OK &&
+                 can_pair(el, er);
+    }
+    if (paired) {
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, 2 * F, dl, nullptr, &fin, 1, &right->p)))
+            return rc;
+    } else if (right) {
         if (!left->side) {
             SDR_HIP(hipStreamCreateWithFlags(&left->side, hipStreamNonBlocking));
             SDR_HIP(hipEventCreateWithFlags(&left->fork, hipEventDisableTiming));
@@ -1040,8 +1093,10 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         if (rc2) return rc2;
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
-    if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
-    if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
+    if (!paired) {
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
+        if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
+    }
     if (wls) {
         // wls_filter->filter(disp_left, left_small, filtered, disp_right) (stereo_disparity.cpp:31)
         // with filtered_disp.convertTo(CV_32F, 1/16) (:34) and computeDepth (:76-80) in its epilogue
@@ -1112,7 +1167,8 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
         return rc;
     SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
     if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, left->cls_dl.p, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (disp_right && right) SDR_HIP(hipMemcpyAsync(disp_right, left->cls_dr.p, px2 * 2, hipMemcpyDeviceToHost, st));
+    if (disp_right && right)
+        SDR_HIP(hipMemcpyAsync(disp_right, (int16_t*)left->cls_dl.p + px2, px2 * 2, hipMemcpyDeviceToHost, st));
     if (filtered) SDR_HIP(hipMemcpyAsync(filtered, filt, px2 * 2, hipMemcpyDeviceToHost, st));
     if (conf && wls) SDR_HIP(hipMemcpyAsync(conf, dconf, px2 * 4, hipMemcpyDeviceToHost, st));
     SDR_HIP(hipStreamSynchronize(st));
@@ -1148,6 +1204,8 @@ int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) 
     const size_t skip = stage == 0 ? h->path_slack * 2 : stage == 4 ? h->path_lslack * 2 : 0;
     if (!b->p || bytes + skip > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));
+    if (stage == 2 && h->lr_skipped && h->draw.p && h->dlr.p)
+        sdr::launch_mask_cols((const int16_t*)h->draw.p, (int16_t*)h->dlr.p, h->lr_g, h->lr_frames, h->stream);
     SDR_HIP(hipStreamSynchronize(h->stream));
     SDR_HIP(hipMemcpy(dst, (const char*)b->p + skip, bytes, hipMemcpyDeviceToHost));
     return SDR_OK;

@@ -42,7 +42,22 @@ struct Geometry {
     int minX1, W1;      // matched column range [minX1, minX1 + W1)
     int SW2, SH2;       // block half sizes
     int P1, P2;
+    // paired matchers (the class path's left and right matcher in one launch): frames >= split
+    // belong to a second matcher whose parameters differ only in minDisparity (same W1), with the
+    // left and right images swapped (right_matcher->compute(R, L)); split > frames: unpaired
+    int split;
+    int minDb, minX1b;  // the second matcher's minD / minX1
 };
+
+// the geometry of frame f (the paired matcher's minD / minX1 for frames >= split)
+__host__ __device__ inline Geometry frame_geom(const Geometry& g, int f) {
+    Geometry r = g;
+    if (f >= g.split) {
+        r.minD = g.minDb;
+        r.minX1 = g.minX1b;
+    }
+    return r;
+}
 
 // ---- prefilter / cost volume (sdr_cost.hip) ----
 struct Planes {
@@ -129,12 +144,15 @@ void launch_lr_check(const Geometry& g, const int16_t* raw, const uint32_t* keys
 
 void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st);
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
-                      int H, int F, int ftzero, const Planes& pl, hipStream_t st);
+                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split = 1 << 30);
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
 void launch_cost_cn3(const Geometry& g, const CostArgs& a, int F, hipStream_t st);  // pl.cn == 3
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
+// median of the WTA map with columns outside [c0, c1) read as fill (LR check skipped)
+void launch_median3_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st);
+void launch_mask_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st);
 // src may equal dst; out_min (nullable) receives min over each output frame.  median_of
 // (nullable): src is instead the 3x3 median of median_of, computed by the first pass and written
 // to median_out (= src) -- the median filter fused into the labelling

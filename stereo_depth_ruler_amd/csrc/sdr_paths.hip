@@ -232,8 +232,9 @@ constexpr uint32_t kNoWrite = 0xfffffffeu;     // staged row outside this chain'
 constexpr uint32_t kRejected = 0xffffffffu;    // no disp2 candidate
 
 template <int DPL, bool PAD, int NP>
-__global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g, PathLaunch pl,
+__global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g0, PathLaunch pl,
                                                                            SouthWtaArgs a) {
+    const Geometry g = frame_geom(g0, blockIdx.y);
     constexpr int K = DPL / 2;
     constexpr int RB = kSouthRB;
     constexpr int LAB = kSouthLAB;
@@ -477,10 +478,11 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
 // (minS << 16 | bestDisp) per matched pixel is scattered into the row's disp2 keys in LDS by
 // atomicMin on (minS << 16 | 0xffff - x) -- the smallest cost wins, ties to the largest x, as in
 // OpenCV's descending loop with a strict '>' -- then OpenCV's check runs per pixel.
-__global__ __launch_bounds__(256) void k_lr_check(Geometry g, const int16_t* __restrict__ raw,
+__global__ __launch_bounds__(256) void k_lr_check(Geometry g0, const int16_t* __restrict__ raw,
                                                   const uint32_t* __restrict__ keys,
                                                   int16_t* __restrict__ out, size_t fstride,
                                                   int disp12MaxDiff) {
+    const Geometry g = frame_geom(g0, blockIdx.y);
     extern __shared__ uint32_t d2[];  // [W]
     const int y = blockIdx.x, f = blockIdx.y;
     const size_t ro = (size_t)f * fstride + (size_t)y * g.W;

@@ -11,15 +11,22 @@ namespace sdr {
 // ------------------------------------------------------------------------------------------
 // A.10 medianBlur 3x3, replicate border (Devillard's 19-exchange median-of-9 network)
 // ------------------------------------------------------------------------------------------
-// 3x3 median at (x, y) of a frame, BORDER_REPLICATE (medianBlur ksize 3: 19-exchange network)
-__device__ __forceinline__ int median3_at(const int16_t* __restrict__ src, int W, int H, int x, int y) {
+// 3x3 median at (x, y) of a frame, BORDER_REPLICATE (medianBlur ksize 3: 19-exchange network).
+// MASK: columns outside [c0, c1) read as `fill` (the WTA map outside the matched columns, which
+// the LR check would have written as INVALID; used when that check cannot fire)
+template <bool MASK = false>
+__device__ __forceinline__ int median3_at(const int16_t* __restrict__ src, int W, int H, int x, int y,
+                                          int c0 = 0, int c1 = 0, int fill = 0) {
     int p[9];
     const int xs[3] = {max(x - 1, 0), x, min(x + 1, W - 1)};
     const int ys[3] = {max(y - 1, 0), y, min(y + 1, H - 1)};
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) p[i * 3 + j] = src[(size_t)ys[i] * W + xs[j]];
+        for (int j = 0; j < 3; j++) {
+            if (MASK && (xs[j] < c0 || xs[j] >= c1)) p[i * 3 + j] = fill;
+            else p[i * 3 + j] = src[(size_t)ys[i] * W + xs[j]];
+        }
 #define SDR_S(a, b) { int t_ = min(p[a], p[b]); p[b] = max(p[a], p[b]); p[a] = t_; }
     SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 1) SDR_S(3, 4) SDR_S(6, 7)
     SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 3) SDR_S(5, 8) SDR_S(4, 7)
@@ -41,6 +48,39 @@ __global__ __launch_bounds__(256) void k_median3(const int16_t* __restrict__ src
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st) {
     dim3 grid((W + 63) / 64, (H + 3) / 4, F);
     hipLaunchKernelGGL(k_median3, grid, dim3(256), 0, st, src, dst, W, H);
+}
+
+// the column mask of frame f: the matched columns [minX1, minX1 + W1) and INVALID of its matcher
+__global__ __launch_bounds__(256) void k_median3_cols(const int16_t* __restrict__ src,
+                                                      int16_t* __restrict__ dst, Geometry g) {
+    const int W = g.W, H = g.H;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const size_t fo = (size_t)blockIdx.z * W * H;
+    if (x >= W || y >= H) return;
+    const Geometry gf = frame_geom(g, blockIdx.z);
+    dst[fo + (size_t)y * W + x] =
+        (int16_t)median3_at<true>(src + fo, W, H, x, y, gf.minX1, gf.minX1 + gf.W1, (gf.minD - 1) * 16);
+}
+
+void launch_median3_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st) {
+    dim3 grid((g.W + 63) / 64, (g.H + 3) / 4, F);
+    hipLaunchKernelGGL(k_median3_cols, grid, dim3(256), 0, st, src, dst, g);
+}
+
+// src outside each frame's matched columns -> its INVALID (the LR-check stage's map when the check
+// cannot fire)
+__global__ void k_mask_cols(const int16_t* __restrict__ src, int16_t* __restrict__ dst, Geometry g, int F) {
+    const size_t px = (size_t)g.W * g.H, n = px * F;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const Geometry gf = frame_geom(g, (int)(i / px));
+        const int x = (int)(i % g.W);
+        dst[i] = (x < gf.minX1 || x >= gf.minX1 + gf.W1) ? (int16_t)((gf.minD - 1) * 16) : src[i];
+    }
+}
+
+void launch_mask_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st) {
+    hipLaunchKernelGGL(k_mask_cols, dim3(256), dim3(256), 0, st, src, dst, g, F);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -408,3 +408,49 @@ def test_host_pointer_page_locked_buffers(oracle):
         assert np.array_equal(pd, ref) and np.array_equal(px.view(np.uint32), ref_xyz.view(np.uint32))
         assert np.array_equal(m.compute(pl, pr, pd), ref)
     m.close()
+
+
+@pytest.mark.parametrize("paired", [True, False])
+def test_class_device_paired_and_forked(oracle, paired):
+    """sdr_stereo_class_depth_device on a batch of 2 frames: the left and right matcher run as one
+    paired batch when they differ only in minDisparity (the class path's case), on a forked side
+    stream otherwise (here: a right matcher with uniquenessRatio 3) -- both bit-exact against the
+    oracle chain, including the fused convertTo(1/16) + computeDepth epilogue."""
+    import ctypes
+
+    from stereo_depth_ruler_amd._lib import lib
+    from stereo_depth_ruler_amd.ximgproc import createDisparityWLSFilter
+
+    h, w, F = 72, 240, 2
+    pairs = [S.make_pair(h, w, 48, seed=200 + i)[:2] for i in range(F)]
+    m = sdr.StereoSGBM.create(0, 48, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_SGBM_3WAY)
+    rm = sdr.createRightMatcher(m)
+    wls = createDisparityWLSFilter(m)
+    wls.setLambda(8000.0)
+    wls.setSigmaColor(1.1)
+    runiq = 0 if paired else 3
+    rm.setUniquenessRatio(runiq)
+    dev = torch.device("cuda", 0)
+    sl = torch.from_numpy(np.stack([p[0] for p in pairs])).to(dev)
+    sr = torch.from_numpy(np.stack([p[1] for p in pairs])).to(dev)
+    out = torch.empty((F, h, w), dtype=torch.float32, device=dev)
+    filt = torch.empty((F, h, w), dtype=torch.int16, device=dev)
+    xyz = torch.empty((F, h, w, 3), dtype=torch.float32, device=dev)
+    Q = (ctypes.c_double * 16)(*np.asarray(S.REFERENCE_Q, np.float64).ravel())
+    L = lib()
+    assert L.sdr_sgbm_set_stream(m._h, None) == 0
+    assert L.sdr_stereo_class_depth_device(m._h, rm._h, wls._h, sl.data_ptr(), sr.data_ptr(), w, h, F,
+                                           out.data_ptr(), filt.data_ptr(), None, Q, xyz.data_ptr()) == 0
+    torch.cuda.synchronize()
+    q = oracle.wls_params_for_sgbm(0, 48, 5, w, h, 8000.0, 1.1)
+    for i, (gl, gr) in enumerate(pairs):
+        ref_l = oracle.sgbm_compute(gl, gr, oracle.make_params(0, 48, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+        ref_r = oracle.sgbm_compute(gr, gl, oracle.make_params(-47, 48, 5, 600, 2400, 1000000, 63, runiq, 0, 2, 2))
+        ref_f = oracle.wls_filter(ref_l, ref_r, gl, q)
+        ref_o = oracle.disp_to_float(ref_f)
+        assert np.array_equal(filt[i].cpu().numpy(), ref_f), i
+        assert np.array_equal(out[i].cpu().numpy(), ref_o), i
+        ref_xyz = oracle.reproject(ref_o, S.REFERENCE_Q, False)
+        assert np.array_equal(xyz[i].cpu().numpy().view(np.uint32), ref_xyz.view(np.uint32)), i
+    for o in (m, rm, wls):
+        o.close()

@@ -96,7 +96,11 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
     return L;
 }
 
-constexpr int kPathsLA = 16;  // k_paths lookahead (steps)
+// k_paths lookahead (steps).  32 steps at D <= 128 measured slower on the class path's 640x360
+// frames (k_paths 75 -> 82 us for both matchers; C2 unchanged): its E/W chains wait on the
+// memory system (3.4 TB/s over the launch), not on the lookahead.
+template <int DPL>
+constexpr int paths_la() { return 16; }
 // k_paths loads C with the default cache policy: the launch's four directions (and k_south_wta
 // after it) re-read C, and the 212 MB volume of a C2 frame is served partly from the 256 MB
 // Infinity Cache -- non-temporal C loads there measured 274 -> 340 us.
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     // LA steps earlier, so every slot keeps one register across the loop's back edge (a ring
     // of LA slots makes the compiler copy the in-flight loads at the back edge, which waits for
     // all of them)
-    constexpr int LA = kPathsLA;
+    constexpr int LA = paths_la<DPL>();
     constexpr int R = 2 * LA;
     const int lane = threadIdx.x & 63;
     // wave-uniform chain index in an SGPR: all chain control flow stays scalar

@@ -355,6 +355,9 @@ int sdr_show_depth_map(sdr_display* h, const float* xyz, int width, int height, 
 int sdr_disparity_overlay(sdr_display* h, const uint8_t* vis, const uint8_t* left_bgr,
                           size_t left_stride, int width, int height, uint8_t* heat,
                           uint8_t* overlay);
+/* StereoDisplayer::depth_coverage of a host xyz map [H][W][3] (synchronous); read-only like the
+ * reference's: the handle's EMA history and range state are untouched. */
+int sdr_depth_coverage(sdr_display* h, const float* xyz, int width, int height, int col0, double* pct);
 
 /* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);

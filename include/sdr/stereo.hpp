@@ -17,9 +17,12 @@
 // pointers with sdr::Mat::view(...) at zero cost.  Errors throw sdr::Exception (cf. cv::Exception).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -52,6 +55,59 @@ inline void check(int rc) {
     if (rc != SDR_OK) throw Exception(rc, sdr_last_error());
 }
 
+namespace detail {
+// Page-locked blocks are expensive to allocate (the driver pins every page), and the reference's
+// calls return fresh Mats per frame (StereoDisparity::computeDisparity, computeDepth): released
+// blocks are kept here and handed to the next allocation of a similar size (best fit within 2x),
+// up to kPinPoolBytes, so a per-frame Mat costs no pinning after the first frames.  The pool is
+// never destroyed (Mats may outlive static destruction); the process exit releases its blocks.
+struct PinPool {
+    static constexpr size_t kPinPoolBytes = (size_t)512 << 20;
+    std::mutex mu;
+    std::multimap<size_t, void*> free_;
+    size_t held = 0;
+    void* get(size_t n, size_t* got) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto it = free_.lower_bound(n);
+            if (it != free_.end() && it->first <= 2 * n) {
+                void* p = it->second;
+                *got = it->first;
+                held -= it->first;
+                free_.erase(it);
+                return p;
+            }
+        }
+        void* p = nullptr;
+        if (sdr_host_alloc(n, &p) != SDR_OK) return nullptr;
+        *got = n;
+        return p;
+    }
+    void put(void* p, size_t n) {
+        std::lock_guard<std::mutex> lk(mu);
+        free_.emplace(n, p);
+        held += n;
+        while (held > kPinPoolBytes && !free_.empty()) {  // evict the largest blocks first
+            auto it = std::prev(free_.end());
+            held -= it->first;
+            sdr_host_free(it->second);
+            free_.erase(it);
+        }
+    }
+};
+inline PinPool& pin_pool() {
+    static PinPool* pool = new PinPool();
+    return *pool;
+}
+// a page-locked block of at least n bytes (nullptr if page-locked memory is unavailable)
+inline std::shared_ptr<void> pinned_block(size_t n) {
+    size_t got = 0;
+    void* p = pin_pool().get(n, &got);
+    if (!p) return nullptr;
+    return std::shared_ptr<void>(p, [got](void* q) { pin_pool().put(q, got); });
+}
+}  // namespace detail
+
 class Mat {
 public:
     int rows = 0, cols = 0, type = CV_8UC1;
@@ -67,24 +123,31 @@ public:
         m.data = (uint8_t*)p;
         return m;
     }
-    void create(int r, int c, int t) {  // like cv::Mat::create: reallocates only when needed
+    // like cv::Mat::create: reallocates only when the shape or type changes.  The storage is
+    // page-locked (sdr_host_alloc), so the engine's host-pointer calls DMA straight to and from
+    // every Mat the facade allocates -- compute()'s disparity, reprojectImageTo3D's xyz,
+    // computeDisparity's output -- with no staging copy; where page-locked memory is unavailable
+    // (no HIP device) it falls back to ordinary memory, which the engine stages.
+    void create(int r, int c, int t) {
         if (data && r == rows && c == cols && t == type) return;
-        rows = r; cols = c; type = t;
-        step = (size_t)c * elem_size(t);
-        auto v = std::make_shared<std::vector<uint8_t>>((size_t)r * step);
-        data = v->data();
-        store_ = v;
+        alloc(r, c, t, true);
     }
-    // page-locked storage (cv::cuda::HostMem(PAGE_LOCKED).createMatHeader()): the host-pointer
-    // calls DMA straight to and from it instead of staging a copy
+    // explicit page-locked storage (cv::cuda::HostMem(PAGE_LOCKED).createMatHeader()); throws if
+    // it cannot be had
     static Mat page_locked(int r, int c, int t) {
         Mat m;
         m.rows = r; m.cols = c; m.type = t;
         m.step = (size_t)c * elem_size(t);
-        void* p = nullptr;
-        check(sdr_host_alloc(std::max<size_t>((size_t)r * m.step, 1), &p));
-        m.store_ = std::shared_ptr<void>(p, [](void* q) { sdr_host_free(q); });
-        m.data = (uint8_t*)p;
+        auto b = detail::pinned_block(std::max<size_t>((size_t)r * m.step, 1));
+        if (!b) throw Exception(SDR_ERR_NOMEM, std::string("page-locked allocation failed: ") + sdr_last_error());
+        m.store_ = b;
+        m.data = (uint8_t*)b.get();
+        return m;
+    }
+    // ordinary (pageable) storage
+    static Mat pageable(int r, int c, int t) {
+        Mat m;
+        m.alloc(r, c, t, false);
         return m;
     }
     bool empty() const { return !data || rows == 0 || cols == 0; }
@@ -98,6 +161,21 @@ public:
     }
 
 private:
+    void alloc(int r, int c, int t, bool pinned) {
+        rows = r; cols = c; type = t;
+        step = (size_t)c * elem_size(t);
+        const size_t bytes = std::max<size_t>((size_t)r * step, 1);
+        if (pinned) {
+            if (auto b = detail::pinned_block(bytes)) {
+                store_ = b;
+                data = (uint8_t*)b.get();
+                return;
+            }
+        }
+        auto v = std::make_shared<std::vector<uint8_t>>(bytes);
+        data = v->data();
+        store_ = v;
+    }
     std::shared_ptr<void> store_;
 };
 
@@ -208,8 +286,11 @@ inline void convertTo32F(const Mat& disp16, Mat& f, double scale) {
     if (disp16.type != CV_16SC1) throw Exception(SDR_ERR_TYPE, "convertTo32F expects CV_16S");
     f.create(disp16.rows, disp16.cols, CV_32FC1);
     const float a = (float)scale;
-    for (int y = 0; y < disp16.rows; y++)
-        for (int x = 0; x < disp16.cols; x++) f.ptr<float>(y)[x] = (float)disp16.ptr<int16_t>(y)[x] * a;
+    for (int y = 0; y < disp16.rows; y++) {  // a plain loop per row: the compiler vectorises it
+        const int16_t* __restrict__ s = disp16.ptr<int16_t>(y);
+        float* __restrict__ d = f.ptr<float>(y);
+        for (int x = 0; x < disp16.cols; x++) d[x] = (float)s[x] * a;
+    }
 }
 
 inline void reprojectImageTo3D(const Mat& disparity, Mat& xyz, const Mat& Q,
@@ -218,7 +299,7 @@ inline void reprojectImageTo3D(const Mat& disparity, Mat& xyz, const Mat& Q,
     q_of(Q, q);
     Mat f = disparity;
     if (disparity.type == CV_16SC1) {  // OpenCV reads CV_16S values as-is (no 1/16 scaling)
-        f = Mat(disparity.rows, disparity.cols, CV_32FC1);
+        f = Mat::pageable(disparity.rows, disparity.cols, CV_32FC1);
         for (int y = 0; y < disparity.rows; y++)
             for (int x = 0; x < disparity.cols; x++) f.ptr<float>(y)[x] = (float)disparity.ptr<int16_t>(y)[x];
     } else if (disparity.type != CV_32FC1) {
@@ -332,13 +413,13 @@ public:
                                     nullptr, out.data));
         return out;
     }
-    // StereoDisplayer::depth_coverage(depth_map): percent of Z in [0, 12000] in columns >= 80
+    // StereoDisplayer::depth_coverage(depth_map): percent of Z in [0, 12000] in columns >= 80;
+    // read-only (this Display's show_depthMap history is untouched)
     double depth_coverage(const Mat& depth) {
         if (depth.type != CV_32FC3 || depth.step != (size_t)depth.cols * 12)
             throw Exception(SDR_ERR_TYPE, "depth_coverage expects a continuous CV_32FC3 map");
-        Mat scratch(depth.rows, depth.cols, CV_8UC3);
-        double pct = 0, zr[2] = {1000.0, 2000.0};  // a throw-away range state: only the count is used
-        check(sdr_show_depth_map(h_, depth.ptr<float>(0), depth.cols, depth.rows, 3, zr, scratch.data, &pct));
+        double pct = 0;
+        check(sdr_depth_coverage(h_, depth.ptr<float>(0), depth.cols, depth.rows, 80, &pct));
         return pct;
     }
     sdr_display* handle() const { return h_; }

@@ -479,6 +479,17 @@ int sdr_show_depth_map(sdr_display* h, const float* xyz, int W, int H, int chann
     return SDR_OK;
 }
 
+int sdr_depth_coverage(sdr_display* h, const float* xyz, int W, int H, int col0, double* pct) {
+    if (!h || !xyz || !pct) return dfail(SDR_ERR_ARG, "null argument");
+    if (W <= 0 || H <= 0) return dfail(SDR_ERR_ARG, "bad size");
+    SDR_DHIP(hipSetDevice(h->device));
+    int rc;
+    if ((rc = sdr::ensure(h->stage_in, (size_t)W * H * 12))) return rc;
+    SDR_DHIP(hipMemcpyAsync(h->stage_in.p, xyz, (size_t)W * H * 12, hipMemcpyHostToDevice, h->stream));
+    // statistics only: the handle's EMA history and range state are not touched
+    return sdr_depth_coverage_device(h, (const float*)h->stage_in.p, W, H, 1, col0, pct);
+}
+
 int sdr_disparity_overlay(sdr_display* h, const uint8_t* vis, const uint8_t* left_bgr, size_t left_stride,
                           int W, int H, uint8_t* heat, uint8_t* overlay) {
     if (!h || !vis || !left_bgr || (!heat && !overlay)) return dfail(SDR_ERR_ARG, "null argument");

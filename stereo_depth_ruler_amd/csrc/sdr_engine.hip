@@ -1157,22 +1157,27 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     float* f = (float*)left->cls_f.p;
     int16_t* filt = (int16_t*)left->cls_filt.p;
     float* dconf = conf ? (float*)left->cls_conf.p : nullptr;
-    SDR_HIP(hipMemcpy2DAsync(bgr, (size_t)W * 3, bgr_left, bgr_stride, (size_t)W * 3, H, hipMemcpyHostToDevice, st));
-    SDR_HIP(hipMemcpy2DAsync(bgr + px * 3, (size_t)W * 3, bgr_right, bgr_stride, (size_t)W * 3, H,
-                             hipMemcpyHostToDevice, st));
+    // host copies through the handle's page-locked staging (DMA straight from/to sdr_host_alloc
+    // buffers, e.g. the facade's Mats)
+    if ((rc = left->hx.begin(2 * stage_bytes(px * 3) + stage_bytes(px2 * 4) * 3 + stage_bytes(px2 * 2) * 3)))
+        return rc;
+    if ((rc = left->hx.upload(bgr, (size_t)W * 3, bgr_left, bgr_stride, (size_t)W * 3, H, st))) return rc;
+    if ((rc = left->hx.upload(bgr + px * 3, (size_t)W * 3, bgr_right, bgr_stride, (size_t)W * 3, H, st))) return rc;
     // cvtColor(BGR2GRAY) x2, resize(0.5, INTER_AREA) x2 (stereo_disparity.cpp:19-24)
     sdr::launch_bgr2gray(bgr, W, H, (size_t)W * 3, gray, W, 2, st);
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
     if ((rc = class_enqueue(left, right, wls, small, small + px2, w2, h2, 1, f, filt, dconf, nullptr, nullptr)))
         return rc;
-    SDR_HIP(hipMemcpy2DAsync(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, hipMemcpyDeviceToHost, st));
-    if (disp_left) SDR_HIP(hipMemcpyAsync(disp_left, left->cls_dl.p, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (disp_right && right)
-        SDR_HIP(hipMemcpyAsync(disp_right, (int16_t*)left->cls_dl.p + px2, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (filtered) SDR_HIP(hipMemcpyAsync(filtered, filt, px2 * 2, hipMemcpyDeviceToHost, st));
-    if (conf && wls) SDR_HIP(hipMemcpyAsync(conf, dconf, px2 * 4, hipMemcpyDeviceToHost, st));
-    SDR_HIP(hipStreamSynchronize(st));
-    return SDR_OK;
+    HostXfer& hx = left->hx;
+    if ((rc = hx.download(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, st))) return rc;
+    if (disp_left && (rc = hx.download(disp_left, (size_t)w2 * 2, left->cls_dl.p, (size_t)w2 * 2, (size_t)w2 * 2, h2, st)))
+        return rc;
+    if (disp_right && right &&
+        (rc = hx.download(disp_right, (size_t)w2 * 2, (int16_t*)left->cls_dl.p + px2, (size_t)w2 * 2, (size_t)w2 * 2, h2, st)))
+        return rc;
+    if (filtered && (rc = hx.download(filtered, (size_t)w2 * 2, filt, (size_t)w2 * 2, (size_t)w2 * 2, h2, st))) return rc;
+    if (conf && wls && (rc = hx.download(conf, (size_t)w2 * 4, dconf, (size_t)w2 * 4, (size_t)w2 * 4, h2, st))) return rc;
+    return hx.drain();
 }
 
 int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int* count) {

@@ -72,6 +72,16 @@ int main(int argc, char** argv) {
                 std::printf("coverage=%.17g\n", disp_out.depth_coverage(depth));
             }
         }
+        // the displayer's order on ONE Display: show_depthMap, depth_coverage, show_depthMap -- the
+        // coverage call must leave the depth map's EMA history alone
+        {
+            sdr::Display dd;
+            double zr[2] = {1000.0, 2000.0};
+            for (int k = 0; k < 2; k++) {
+                dump(out + "/dd_depthvis" + std::to_string(k) + ".bin", dd.show_depthMap(depth, zr));
+                std::printf("dd_coverage%d=%.17g\n", k, dd.depth_coverage(depth));
+            }
+        }
         std::printf("numDisparities=%d\n", sd.get_matcher()->getNumDisparities());
         // error behaviour: numDisparities not divisible by 16 -> exception, like cv::Exception
         try {

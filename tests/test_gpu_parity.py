@@ -348,8 +348,17 @@ def test_cpp_facade(oracle, tmp_path):
     small = oracle.resize_area_half_bgr(bl)
     ov = oracle.add_weighted(small, 0.7, oracle.apply_colormap(pv, jet), 0.3)
     assert np.array_equal(np.fromfile(tmp_path / "overlay.bin", np.uint8).reshape(h2, w2, 3), ov)
-    cov = float(res.stdout.split("coverage=")[1].split()[0])
+    cov = float(res.stdout.split("\ncoverage=")[1].split()[0])
     assert cov == oracle.depth_coverage(depth, 80)
+    # one Display through show_depthMap -> depth_coverage -> show_depthMap: the second
+    # map blends against the first, as with no coverage call in between
+    zr = np.array([1000.0, 2000.0])
+    pd = None
+    for k in range(2):
+        dv = oracle.show_depth_map(depth, zr, turbo, pd)
+        assert np.array_equal(np.fromfile(tmp_path / f"dd_depthvis{k}.bin", np.uint8).reshape(h2, w2, 3), dv), k
+        assert float(res.stdout.split(f"dd_coverage{k}=")[1].split()[0]) == oracle.depth_coverage(depth, 80)
+        pd = dv
 
 
 def test_host_pointer_strides_and_sizes(oracle):

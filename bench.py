@@ -81,8 +81,9 @@ def cpu_baseline(cfg, seconds_target=15.0):
     on a bounded sample of the same workload, two ways:
       throughput -- one frame per thread, `threads` frames at a time (ctypes releases the GIL);
       latency    -- one thread, one frame at a time (OpenCV's SGBM/HH run single-threaded).
-    threads = this GPU's share of the host: OMP_NUM_THREADS (16 per GPU on the GPU box, whose
-    nproc shows the whole machine), else every CPU the process may run on."""
+    threads = this GPU's share of the host: nproc / 8 (one of the node's 8 GPUs; nproc shows the
+    whole machine on the GPU box), capped by OMP_NUM_THREADS when the driver's policy sets it
+    lower (the box sets 16 against nproc / 8 = 32); `host.policy` says which applies."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle as O
@@ -90,8 +91,12 @@ def cpu_baseline(cfg, seconds_target=15.0):
 
     _, W, H, args, _, hm, kind = cfg
     model, ncpu = host_cpu()
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = max(1, min(share, ncpu) if share > 0 else ncpu)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    gpu_share = max(1, ncpu // 8)
+    if omp > 0 and omp < gpu_share:
+        threads, policy = omp, f"OMP_NUM_THREADS={omp} (driver policy) is below nproc/8={gpu_share}: {omp} threads"
+    else:
+        threads, policy = gpu_share, f"nproc/8 = {gpu_share} threads (one of the node's 8 GPUs' share of the host)"
     p = O.make_params(*args)
     if kind == "sgbm":
         L, R, _ = S.make_pair(H, W, args[1], seed=12345)
@@ -158,7 +163,7 @@ def cpu_baseline(cfg, seconds_target=15.0):
         "latency": {"ms_per_frame": round(lat_s * 1e3, 2), "value": round(W * H / lat_s / 1e6, 4),
                     "unit": "Mpix/s", "threads": 1, "frames": len(lat)},
         "host": {"cpu_model": model, "nproc": ncpu, "threads_used": threads,
-                 "omp_num_threads": share or None},
+                 "omp_num_threads": omp or None, "policy": policy},
     }
 
 

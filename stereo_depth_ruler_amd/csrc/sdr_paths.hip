@@ -289,15 +289,17 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         const int naux = pd.Caux ? pd.aux_rows : 0;
         const char* abase = pd.Caux ? (const char*)(pd.Caux + (size_t)f * pl.aux_fstride + (size_t)ch.x0 * D)
                                     : (const char*)pl.C;
-        const char* cp = (const char*)(pl.C + fofs + ((size_t)ch.y0 * W1 + ch.x0) * D);  // row k + LA
+        const char* c0 = (const char*)(pl.C + fofs + ((size_t)ch.y0 * W1 + ch.x0) * D);
         // a resource per load: the compiler then bunches the loads into one burst per block
-        // (measured faster than one resource per chain with an SGPR row offset here)
+        // (measured faster than one resource per chain with an SGPR row offset here).  Rows past
+        // the chain's end re-read its last row (an L2 hit) instead of the buffer's slack rows:
+        // the class path's 3WAY stripes are ~100 rows, and a lookahead of LA rows past each
+        // stripe's end was a quarter of the pass's HBM reads there
+        auto crow = [&](int k) { return c0 + (ptrdiff_t)min(k, last) * rowb; };
         Regs<K> cring[R];
 #pragma unroll
-        for (int j = 0; j < LA; j++) {
-            cring[j] = load_buf<K>(rsrc_at(j < naux ? abase + (ptrdiff_t)j * rowb : cp), lofs);
-            cp += rowb;
-        }
+        for (int j = 0; j < LA; j++)
+            cring[j] = load_buf<K>(rsrc_at(j < naux ? abase + (ptrdiff_t)j * rowb : crow(j)), lofs);
         Regs<K> Lp;
 #pragma unroll
         for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
@@ -310,8 +312,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             auto st = [&](const int, auto jc) __attribute__((always_inline)) {
                 constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
                 const Regs<K> c = cring[j];
-                cring[(j + LA) % R] = load_buf<K, kLoadNT>(rsrc_at(cp), lofs);
-                cp += rowb;
+                cring[(j + LA) % R] = load_buf<K, kLoadNT>(rsrc_at(crow(bb * RB + (j % RB) + LA)), lofs);
                 const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
 #pragma unroll
                 for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];
@@ -342,8 +343,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         lofs[ps] = (uint32_t)(((size_t)rr[ps] * W1 * pl.l_pix + wd0) * 2);
     }
     const char* lbase = (const char*)(a.L + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
+    // blocks past the chain's last one re-read that block (L2 hits), not the buffers' slack
     auto oload = [&](int q, int blk, int ps) __attribute__((always_inline)) {
-        return load_buf<WK, kLoadNT>(rsrc_at(lbase + (ptrdiff_t)blk * bstepb), lofs[ps] + (uint32_t)(q * D * 2));
+        return load_buf<WK, kLoadNT>(rsrc_at(lbase + (ptrdiff_t)min(blk, nblk - 1) * bstepb),
+                                     lofs[ps] + (uint32_t)(q * D * 2));
     };
     // rows before kw belong to the previous 3WAY stripe: recurred through, never output
     const int kw = ch.kwrite;
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     // ring of PD blocks: slot s holds block b (b = s mod PD) until its sum is taken, then the
     // load of block b + PD goes into the same registers, so each block's loads have PD block
     // periods to land (the loop is unrolled by PD: static slots, no copies at the back edge);
-    // unconditional: blocks past the chain's end read the buffers' row slack (kSouthPad)
+    // unconditional: blocks past the chain's end re-read its last block (oload clamps)
     Regs<WK> oring[PD][NPASS][NP];
 #pragma unroll
     for (int s = 0; s < PD; s++)

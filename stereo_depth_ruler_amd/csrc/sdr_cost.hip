@@ -77,14 +77,16 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 int xx = x + k - 1;
+                // OpenCV's clip table is uchar: past preFilterCap 127 its entries (and the border's
+                // tab[0] = ftzero past 255) wrap mod 256
                 if (xx <= 0 || xx >= W - 1) {
-                    sv[k] = ftzero;
-                    rv[k] = ftzero;
+                    sv[k] = ftzero & 0xff;
+                    rv[k] = ftzero & 0xff;
                 } else {
                     const int a = (xx + 1) * cn + ch, b = (xx - 1) * cn + ch;
                     int gr = 2 * (r[a] - r[b]) + n[a] - n[b] + s[a] - s[b];
                     gr = gr < -ftzero ? -ftzero : (gr > ftzero ? ftzero : gr);
-                    sv[k] = gr + ftzero;
+                    sv[k] = (gr + ftzero) & 0xff;
                     rv[k] = r[xx * cn + ch];
                 }
             }

@@ -361,7 +361,12 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
             slots = max(1, cus * max(1, per_cu));
             key = lds;
         }
-        const int bands = max(1, slots / max(1, colblocks * F));
+        // the 3WAY stripe-start bands are extra rows of blocks in the same launch: leave them
+        // their slots, or the launch spills into a second pass (C4: 828 blocks on 768 slots,
+        // 61 -> 35 us)
+        const int per_band = max(1, colblocks * F);
+        const int avail = max(per_band, slots - a.naux * per_band);
+        const int bands = max(1, avail / per_band);
         a.TY = max(4, (rows + bands - 1) / bands);
     }
     if (rows == 0) a.TY = 1;

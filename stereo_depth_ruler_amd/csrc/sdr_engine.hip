@@ -74,9 +74,7 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     e->uniq = p.uniquenessRatio >= 0 ? p.uniquenessRatio : 10;
     if (e->uniq >= 100) return fail(SDR_ERR_ARG, "uniquenessRatio must be < 100");
     e->disp12MaxDiff = p.disp12MaxDiff > 0 ? p.disp12MaxDiff : 1;
-    e->ftzero = std::max(p.preFilterCap, 15) | 1;
-    // OpenCV's clip table is uchar: past 127 its 2*ftzero entries wrap mod 256
-    if (e->ftzero > 127) return fail(SDR_ERR_LIMIT, "preFilterCap > 127 is not supported");
+    e->ftzero = std::max(p.preFilterCap, 15) | 1;  // any size: the clip table wraps mod 256 (k_prefilter)
     e->nstripes = p.nstripes > 0 ? p.nstripes : 4;
     e->uniq_simd = p.uniq_rule == SDR_UNIQ_SIMD ? 1
                  : p.uniq_rule == SDR_UNIQ_SCALAR ? 0
@@ -90,7 +88,9 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     // (minLp <= C) must fit a short.  Past it OpenCV's SIMD build wraps (short)delta0 and
     // saturates C while its scalar build computes them in int, so the reference's output is not
     // defined by the algorithm alone; the engine refuses instead of picking one of the two.
-    const long bmax = (long)(2 * e->ftzero + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
+    // the largest pixel cost: BT of the prefiltered channel (values in [0, min(2*ftzero, 255)],
+    // the uchar clip table) + BT of the raw one >> 2
+    const long bmax = (long)(std::min(2 * e->ftzero, 255) + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
     if (2L * g.P2 + bmax > 32767)
         return fail(SDR_ERR_LIMIT, "2*P2 + (2*preFilterCap+63)*blockSize^2 exceeds the int16 cost "
                                    "range (OpenCV's SIMD and scalar builds disagree there)");
@@ -124,7 +124,7 @@ int check_channels(const Eff& e, int cn) {
     if (cn != 1 && cn != 3) return fail(SDR_ERR_TYPE, "images must have 1 or 3 channels");
     if (cn == 1) return SDR_OK;
     const sdr::Geometry& g = e.g;
-    const long bmax = (long)cn * (2 * e.ftzero + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
+    const long bmax = (long)cn * (std::min(2 * e.ftzero, 255) + 63) * (2 * g.SW2 + 1) * (2 * g.SH2 + 1);
     if (2L * g.P2 + bmax > 32767)
         return fail(SDR_ERR_LIMIT, "2*P2 + 3*(2*preFilterCap+63)*blockSize^2 exceeds the int16 cost "
                                    "range (OpenCV's SIMD and scalar builds disagree there)");

@@ -4,15 +4,16 @@ import numpy as np
 
 
 def prefilter_channels(img, ftzero):
-    """x-Sobel clipped to [0, 2*ftzero] and raw intensity; cols 0 / W-1 = ftzero (tab[0])."""
+    """x-Sobel clipped to [0, 2*ftzero] and raw intensity; cols 0 / W-1 = ftzero (tab[0]).  The
+    clip table holds uchar values: past preFilterCap 127 they wrap mod 256."""
     I = img.astype(np.int32)
     H, W = I.shape
     up = np.vstack([I[:1], I[:-1]])
     dn = np.vstack([I[1:], I[-1:]])
-    sob = np.full((H, W), ftzero, np.int32)
-    raw = np.full((H, W), ftzero, np.int32)
+    sob = np.full((H, W), ftzero & 0xff, np.int32)
+    raw = np.full((H, W), ftzero & 0xff, np.int32)
     g = 2 * (I[:, 2:] - I[:, :-2]) + (up[:, 2:] - up[:, :-2]) + (dn[:, 2:] - dn[:, :-2])
-    sob[:, 1:-1] = np.clip(g, -ftzero, ftzero) + ftzero
+    sob[:, 1:-1] = (np.clip(g, -ftzero, ftzero) + ftzero) & 0xff
     raw[:, 1:-1] = I[:, 1:-1]
     return sob, raw
 

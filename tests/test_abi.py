@@ -133,8 +133,9 @@ def test_int16_domain_guard_host_only():
         bad = _lib.SgbmParams(0, 64, bs, 10, pmax + 1, 1, cap, 10, 0, 0, mode, 4, 0)
         assert L.sdr_sgbm_scratch_bytes(ctypes.byref(bad), 320, 100, 1) == 0
         assert b"int16" in L.sdr_last_error()
-    big = _lib.SgbmParams(0, 64, 5, 10, 100, 1, 128, 10, 0, 0, 0, 4, 0)
-    assert L.sdr_sgbm_scratch_bytes(ctypes.byref(big), 320, 100, 1) == 0  # preFilterCap > 127
+    for cap in (128, 255, 1000):  # OpenCV accepts any preFilterCap (its uchar clip table wraps)
+        big = _lib.SgbmParams(0, 64, 5, 10, 100, 1, cap, 10, 0, 0, 0, 4, 0)
+        assert L.sdr_sgbm_scratch_bytes(ctypes.byref(big), 320, 100, 1) > 0
 
 
 def test_chain_span_guard_host_only():

@@ -47,7 +47,8 @@ def sgbm_cases(draw):
     H = draw(st.integers(4, 48))
     W1 = draw(st.integers(bs // 2 + 1, 160))  # matched columns (0 < W1 <= SW2 is an OpenCV error)
     W = W1 - min(minD, 0) + max(minD + D, 0)
-    cap = draw(st.sampled_from([c for c in (15, 31, 63, 127) if p2_domain_max(bs, c, mode) >= 64]))
+    cap = draw(st.sampled_from([c for c in (15, 31, 63, 127, 128, 200, 255, 300)
+                                if p2_domain_max(bs, c, mode) >= 64]))
     pmax = p2_domain_max(bs, cap, mode)
     P1 = draw(st.integers(1, max(1, min(pmax - 1, 2000))))
     P2 = draw(st.one_of(st.just(pmax), st.integers(P1 + 1, max(P1 + 1, pmax))))

@@ -66,6 +66,9 @@ CASES = [
     (33, 100, 16, 3, 5, 0, 12, (20, 2), 1, 600, 2400, 63, 21),          # MODE_HH4 (4 paths)
     (48, 200, 128, 3, 3, -6, 10, (0, 0), 1, 300, 1800, 31, 22),         # MODE_HH4, minD < 0
     (40, 320, 208, 3, 7, 0, 5, (50, 2), 2, 100, 900, 15, 23),           # MODE_HH4, D > 128
+    (48, 200, 64, 0, 5, 0, 10, (50, 2), 1, 300, 1800, 200, 24),         # preFilterCap > 127 (uchar wrap)
+    (40, 180, 48, 2, 3, -4, 12, (0, 0), 1, 600, 2400, 255, 25),         # 3WAY, cap 255
+    (36, 160, 32, 1, 5, 0, 10, (20, 2), 1, 200, 900, 1000, 26),         # MODE_HH, ftzero 1001 (tab[0] wraps)
 ]
 
 

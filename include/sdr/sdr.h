@@ -359,8 +359,13 @@ int sdr_disparity_overlay(sdr_display* h, const uint8_t* vis, const uint8_t* lef
  * reference's: the handle's EMA history and range state are untouched. */
 int sdr_depth_coverage(sdr_display* h, const float* xyz, int width, int height, int col0, double* pct);
 
-/* Bytes of device scratch the handle holds for the given frame shape (for capacity planning). */
+/* Bytes of device scratch the handle holds for the given frame shape (for capacity planning);
+ * 0 when compute would refuse the shape or parameters.  sdr_sgbm_scratch_bytes is the CV_8UC1
+ * figure, sdr_sgbm_scratch_bytes_cn takes the channel count (1 or 3: colour input holds three
+ * operand sets per image). */
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes);
+size_t sdr_sgbm_scratch_bytes_cn(const sdr_sgbm_params* p, int width, int height, int channels,
+                                 int nframes);
 
 /* Timing with HIP events on the handle's stream.  level 1: per-stage timing of the last compute
  * (sdr_sgbm_last_timing: cost volume / path aggregation / LR+median+speckle, ms).  level 2 also
@@ -382,10 +387,12 @@ int sdr_selftest_wave_ops(int* failures4);
 
 /* Diagnostics: synchronously copy an internal buffer of the last compute to host memory.
  * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,
- * 2 = after the LR check, 3 = final (median + speckle), 4 = path costs L [P-1][F][H][W1][D] s16
- * (every direction but top-to-bottom, whose L is consumed on chip by the fused WTA pass),
- * 5 = the fused WTA pass's per-pixel (minS << 16 | bestDisp) [F][H][W] u32, indexed by matched
- * column (0xffffffff: rejected); stage 1 holds values only in the matched columns. */
+ * 2 = after the LR check (computed from stages 1 and 5 on request: the pipeline's median computes
+ * it per tile and never writes it), 3 = final (median + speckle), 4 = path costs L
+ * [P-1][F][H][W1][D] s16 (every direction but top-to-bottom, whose L is consumed on chip by the
+ * fused WTA pass), 5 = the right view's WTA keys [F][H][W] u32: (minS << 16 | 0xffff - x) of the
+ * winning left pixel x (matched column) per right-view column, 0xffffffff where none (not built
+ * when the LR check cannot fire); stage 1 holds values only in the matched columns. */
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
 
 /* Page-locked host memory (the role of cv::cuda::HostMem): host buffers from sdr_host_alloc that

@@ -146,6 +146,7 @@ SIGNATURES = [
     ("sdr_disparity_overlay", _i, [_vp, _vp, _vp, _sz, _i, _i, _vp, _vp]),
     ("sdr_depth_coverage", _i, [_vp, _vp, _i, _i, _i, _c.POINTER(_c.c_double)]),
     ("sdr_sgbm_scratch_bytes", _sz, [_PP, _i, _i, _i]),
+    ("sdr_sgbm_scratch_bytes_cn", _sz, [_PP, _i, _i, _i, _i]),
     ("sdr_sgbm_enable_timing", _i, [_vp, _i]),
     ("sdr_sgbm_last_timing", _i, [_vp, _c.POINTER(_c.c_float), _c.POINTER(_c.c_float),
                                   _c.POINTER(_c.c_float)]),

@@ -57,13 +57,18 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
              "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines] + list(extra)
     hipcc = _hipcc()
     objs, procs = [], []
+    hdr_t = max(os.path.getmtime(d) for d in [os.path.join(CSRC, h) for h in HEADERS] +
+                [os.path.join(ROOT, "include", "sdr", "sdr.h")])
     for f in SOURCES:
         obj = os.path.join(objdir, f.replace(".hip", ".o"))
+        objs.append(obj)
+        # an object newer than its source and every header is reused (same flags: one objdir per variant)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, f))):
+            continue
         cmd = [hipcc, *flags, "-c", os.path.join(CSRC, f), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append((cmd, subprocess.Popen(cmd)))
-        objs.append(obj)
     failed = [cmd for cmd, p in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])

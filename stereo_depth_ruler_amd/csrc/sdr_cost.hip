@@ -46,7 +46,7 @@ void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st) {
 __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ Limg,
                                                    const uint8_t* __restrict__ Rimg, size_t stride,
                                                    size_t fstride, int W, int H, int ftzero,
-                                                   Planes pl, int split) {
+                                                   Planes pl, int split, uint32_t* d2fill) {
     extern __shared__ uint64_t q6[];  // [W] 6 bytes per pixel, then the 3 input rows [3][W*cn] bytes
     const int y = blockIdx.x, img = blockIdx.y, f = blockIdx.z;
     const int cn = pl.cn, WB = W * cn;
@@ -66,6 +66,11 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
             rows[2 * WB + x] = gs[x];
         }
         __syncthreads();
+    }
+    if (d2fill && img == 0) {
+        // the right-view keys of this row start empty (k_south_wta's atomics fold into them)
+        uint32_t* d2 = d2fill + ((size_t)f * H + y) * W;
+        for (int x = threadIdx.x; x < W; x += blockDim.x) d2[x] = kD2None;
     }
     const uint8_t* n = (const uint8_t*)(q6 + W);
     const uint8_t* r = n + WB;
@@ -132,9 +137,10 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
 }
 
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
-                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split) {
+                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split,
+                      uint32_t* d2fill) {
     hipLaunchKernelGGL(k_prefilter, dim3(H, 2, F), dim3(256), (size_t)W * (8 + 3 * pl.cn), st, L, R,
-                       stride, fstride, W, H, ftzero, pl, split);
+                       stride, fstride, W, H, ftzero, pl, split, d2fill);
 }
 
 }  // namespace sdr

@@ -341,7 +341,7 @@ struct sdr_sgbm {
     // rebuilt on request from the WTA map with this geometry
     bool lr_skipped = false;
     sdr::Geometry lr_g{};
-    int lr_frames = 0;
+    int lr_frames = 0, lr_d12 = 0;
 };
 
 namespace {
@@ -383,7 +383,7 @@ struct KTimer {
 
 static int npaths_of(int mode);
 
-static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
+static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st, int cn) {
     const sdr::Geometry& g = e.g;
     const size_t cells = (size_t)g.H * std::max(g.W1, 0) * g.D;
     size_t aux = 0;
@@ -394,7 +394,7 @@ static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st) {
         aux = (size_t)st->size() * amax * std::max(g.W1, 0) * g.D * 2;
     }
     const size_t px = (size_t)g.W * g.H;
-    return (size_t)F * (3 * px * 4 + 3 * px * 8 + cells * 2 * npaths_of(e.mode) + aux + px * 2 * 3 + px * 4 +
+    return (size_t)F * (3 * px * 4 * cn + 3 * px * 8 * cn + cells * 2 * npaths_of(e.mode) + aux + px * 2 * 3 + px * 4 +
                         px * 4 * 2);
 }
 
@@ -485,14 +485,24 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     int16_t* Caux = (int16_t*)h->Caux.p;
     int16_t* Lr = (int16_t*)h->Lr.p + lslack;  // [F][H][W1][P-1][D]
     int16_t* draw = (int16_t*)h->draw.p;
-    int16_t* dlr = (int16_t*)h->dlr.p;
 
     sdr::Planes pl;
     pl.L = (uint32_t*)h->planesL.p;
     pl.R = (uint64_t*)h->planesR.p;
     pl.fstrideL = pl.fstrideR = 3 * px * cn;
     pl.cn = cn;
-    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st, g.split); }
+    const bool speckle = e.speckle_ws > 0;
+    // A.9 can only invalidate a pixel when |disp2 - d| > disp12MaxDiff; both lie in [minD, maxD),
+    // so from disp12MaxDiff >= D on (ximgproc's WLS filter sets 1000000 on the class path's left
+    // matcher, createRightMatcher on the right one) the check is the identity on the matched
+    // columns and INVALID elsewhere: the median reads the WTA map with that column mask instead,
+    // and no right-view keys are built
+    h->lr_skipped = !speckle && e.disp12MaxDiff >= g.D;
+    h->lr_g = g;
+    h->lr_frames = F;
+    h->lr_d12 = e.disp12MaxDiff;
+    uint32_t* d2 = h->lr_skipped ? nullptr : (uint32_t*)h->keys2.p;
+    { KTimer kt(h, SDR_KERNEL_PREFILTER); sdr::launch_prefilter(L, R, stride, fstride, W, H, F, e.ftzero, pl, st, g.split, d2); }
 
     sdr::CostArgs ca{};
     ca.pl = pl;
@@ -588,33 +598,23 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     wa.L = Lr;
     wa.npaths = P;
     wa.disp_raw = draw;
-    wa.keys2 = (uint32_t*)h->keys2.p;
+    wa.d2 = d2;
     wa.disp_fstride = px;
     wa.uniq = e.uniq;
     wa.uniq_simd = e.uniq_simd;
     { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
-    const bool speckle = e.speckle_ws > 0;
-    // A.9 can only invalidate a pixel when |disp2 - d| > disp12MaxDiff; both lie in [minD, maxD),
-    // so from disp12MaxDiff >= D on (ximgproc's WLS filter sets 1000000 on the class path's left
-    // matcher, createRightMatcher on the right one) the check is the identity on the matched
-    // columns and INVALID elsewhere: the median reads the WTA map with that column mask instead
-    h->lr_skipped = !speckle && e.disp12MaxDiff >= g.D;
-    h->lr_g = g;
-    h->lr_frames = F;
-    if (!h->lr_skipped) {
-        KTimer kt(h, SDR_KERNEL_LR_CHECK);
-        sdr::launch_lr_check(g, draw, wa.keys2, dlr, px, e.disp12MaxDiff, F, st);
-    }
+    const sdr::LrSrc lr{g, draw, d2, px, e.disp12MaxDiff};
     if (speckle) {
-        // the median filter runs inside the labelling's first pass (dfin = median of dlr)
+        // the LR check and the median filter run inside the labelling's first pass (dfin = median
+        // of the LR-checked map, computed per tile from draw and d2)
         KTimer kt(h, SDR_KERNEL_SPECKLE);
         sdr::launch_speckle(dfin, dst, W, H, F, e.invalid, e.speckle_ws, e.speckle_diff,
-                            (int*)h->labels.p, (int*)h->sizes.p, out_min, st, dlr, dfin);
+                            (int*)h->labels.p, (int*)h->sizes.p, out_min, st, &lr, dfin);
     } else {
         {
             KTimer kt(h, SDR_KERNEL_MEDIAN);
             if (h->lr_skipped) sdr::launch_median3_cols(draw, dst, g, F, st);
-            else sdr::launch_median3(dlr, dst, W, H, F, st);
+            else sdr::launch_median3_lr(lr, dst, F, st);
         }
         if (out_min) {
             KTimer kt(h, SDR_KERNEL_REPROJECT);
@@ -754,11 +754,26 @@ int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, flo
 }
 
 size_t sdr_sgbm_scratch_bytes(const sdr_sgbm_params* p, int width, int height, int nframes) {
+    return sdr_sgbm_scratch_bytes_cn(p, width, height, 1, nframes);
+}
+
+size_t sdr_sgbm_scratch_bytes_cn(const sdr_sgbm_params* p, int width, int height, int channels,
+                                 int nframes) {
     if (!p) return 0;
     Eff e;
-    if (make_eff(*p, width, height, &e) || check_frame(e)) return 0;
+    if (make_eff(*p, width, height, &e) || check_channels(e, channels) || check_frame(e)) return 0;
     std::vector<Stripe> st;
-    return scratch_bytes(e, std::max(nframes, 1), &st);
+    return scratch_bytes(e, std::max(nframes, 1), &st, channels);
+}
+
+// Everything enqueue_compute refuses, checked before a host-pointer call stages or uploads
+// anything (an error return then leaves no DMA in flight from the staging buffer).
+static int precheck(const sdr_sgbm* h, int W, int H, int cn) {
+    Eff e;
+    int rc = make_eff(h->p, W, H, &e);
+    if (rc) return rc;
+    if ((rc = check_channels(e, cn))) return rc;
+    return e.g.W1 > 0 ? check_frame(e) : SDR_OK;
 }
 
 static int check_dims(int W, int H, size_t stride, int F) {
@@ -830,6 +845,7 @@ int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int
     int rc = check_dims(W * cn, H, stride, 1);
     if (rc) return rc;
     if (disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
+    if ((rc = precheck(h, W, H, cn))) return rc;
     SDR_HIP(hipSetDevice(h->device));
     const size_t px = (size_t)W * H, ib = px * cn;
     if ((rc = ensure(h->hin, 2 * ib))) return rc;
@@ -839,7 +855,10 @@ int sdr_sgbm_compute(sdr_sgbm* h, const uint8_t* left, const uint8_t* right, int
     if ((rc = h->hx.upload(dL, (size_t)W * cn, left, stride, (size_t)W * cn, H, h->stream))) return rc;
     if ((rc = h->hx.upload(dR, (size_t)W * cn, right, stride, (size_t)W * cn, H, h->stream))) return rc;
     int16_t* fin = nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, (size_t)W * cn, ib, 1, nullptr, nullptr, &fin, cn))) return rc;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, (size_t)W * cn, ib, 1, nullptr, nullptr, &fin, cn))) {
+        (void)hipStreamSynchronize(h->stream);  // the uploads from the staging buffer have landed
+        return rc;
+    }
     if ((rc = h->hx.download(disp, disp_stride * 2, fin, (size_t)W * 2, (size_t)W * 2, H, h->stream))) return rc;
     return h->hx.drain();
 }
@@ -852,6 +871,7 @@ int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* 
     if (rc) return rc;
     if (disp && disp_stride < (size_t)W) return fail(SDR_ERR_ARG, "disp_stride < width");
     if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
+    if ((rc = precheck(h, W, H, 1))) return rc;
     SDR_HIP(hipSetDevice(h->device));
     const size_t px = (size_t)W * H;
     if ((rc = ensure(h->hin, 2 * px))) return rc;
@@ -865,7 +885,10 @@ int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* 
     if ((rc = h->hx.upload(dR, W, right, stride, W, H, h->stream))) return rc;
     int16_t* fin = nullptr;
     int* mins = handle_missing ? (int*)h->mins.p : nullptr;
-    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, mins, &fin))) return rc;
+    if ((rc = enqueue_compute(h, dL, dR, W, H, W, px, 1, nullptr, mins, &fin))) {
+        (void)hipStreamSynchronize(h->stream);  // the uploads from the staging buffer have landed
+        return rc;
+    }
     // the disparity's copy-out overlaps the reprojection
     if (disp && (rc = h->hx.download(disp, disp_stride * 2, fin, (size_t)W * 2, (size_t)W * 2, H, h->stream)))
         return rc;
@@ -1141,10 +1164,11 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     if ((W & 1) || (H & 1)) return fail(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
     const int w2 = W / 2, h2 = H / 2;
     if (out_stride < (size_t)w2) return fail(SDR_ERR_ARG, "out_stride < width/2");
+    int rc;
+    if ((rc = precheck(left, w2, h2, 1)) || (right && (rc = precheck(right, w2, h2, 1)))) return rc;
     SDR_HIP(hipSetDevice(left->device));
     hipStream_t st = left->stream;
     const size_t px = (size_t)W * H, px2 = (size_t)w2 * h2;
-    int rc;
     if ((rc = ensure(left->cls_bgr, 2 * px * 3))) return rc;
     if ((rc = ensure(left->cls_gray, 2 * px))) return rc;
     if ((rc = ensure(left->cls_small, 2 * px2))) return rc;
@@ -1166,8 +1190,10 @@ int sdr_stereo_class_compute(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls,
     // cvtColor(BGR2GRAY) x2, resize(0.5, INTER_AREA) x2 (stereo_disparity.cpp:19-24)
     sdr::launch_bgr2gray(bgr, W, H, (size_t)W * 3, gray, W, 2, st);
     sdr::launch_area_half(gray, W, H, W, small, w2, 2, st);
-    if ((rc = class_enqueue(left, right, wls, small, small + px2, w2, h2, 1, f, filt, dconf, nullptr, nullptr)))
+    if ((rc = class_enqueue(left, right, wls, small, small + px2, w2, h2, 1, f, filt, dconf, nullptr, nullptr))) {
+        (void)hipStreamSynchronize(st);  // the uploads from the staging buffer have landed
         return rc;
+    }
     HostXfer& hx = left->hx;
     if ((rc = hx.download(out, out_stride * 4, f, (size_t)w2 * 4, (size_t)w2 * 4, h2, st))) return rc;
     if (disp_left && (rc = hx.download(disp_left, (size_t)w2 * 2, left->cls_dl.p, (size_t)w2 * 2, (size_t)w2 * 2, h2, st)))
@@ -1209,8 +1235,15 @@ int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) 
     const size_t skip = stage == 0 ? h->path_slack * 2 : stage == 4 ? h->path_lslack * 2 : 0;
     if (!b->p || bytes + skip > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));
-    if (stage == 2 && h->lr_skipped && h->draw.p && h->dlr.p)
-        sdr::launch_mask_cols((const int16_t*)h->draw.p, (int16_t*)h->dlr.p, h->lr_g, h->lr_frames, h->stream);
+    // the LR-checked map is never written by the pipeline: materialise it for this stage
+    if (stage == 2 && h->draw.p && h->dlr.p) {
+        const size_t px = (size_t)h->lr_g.W * h->lr_g.H;
+        if (h->lr_skipped)
+            sdr::launch_mask_cols((const int16_t*)h->draw.p, (int16_t*)h->dlr.p, h->lr_g, h->lr_frames, h->stream);
+        else
+            sdr::launch_lr_apply(h->lr_g, (const int16_t*)h->draw.p, (const uint32_t*)h->keys2.p,
+                                 (int16_t*)h->dlr.p, px, h->lr_d12, h->lr_frames, h->stream);
+    }
     SDR_HIP(hipStreamSynchronize(h->stream));
     SDR_HIP(hipMemcpy(dst, (const char*)b->p + skip, bytes, hipMemcpyDeviceToHost));
     return SDR_OK;

@@ -133,32 +133,71 @@ struct SouthWtaArgs {
     const int16_t* L;             // the P-1 other directions' records, in order, S removed
     int npaths;
     int16_t* disp_raw;   // [F][H][W] WTA disparity (written in the matched columns only)
-    uint32_t* keys2;     // [F][H][W] (minS << 16 | bestDisp) per matched column x (0xffffffff: rejected)
+    // [F][H][W] the right view's WTA keys (A.8's disp2 candidates), null when the LR check cannot
+    // fire: each accepted pixel x (matched-range column) folds (minS << 16 | 0xffff - x) into
+    // x2 = x + minX1 - bestDisp - minD by atomicMin (the smallest cost wins, ties to the largest
+    // x, as OpenCV's descending loop with a strict '>'); k_prefilter fills it with kD2None
+    uint32_t* d2;
     size_t disp_fstride;
     int uniq, uniq_simd;
 };
 void launch_south_wta(const Geometry& g, const PathLaunch& pl, const SouthWtaArgs& a, int F,
                       hipStream_t st);
-void launch_lr_check(const Geometry& g, const int16_t* raw, const uint32_t* keys, int16_t* out,
+
+// A.9, OpenCV's disp12MaxDiff check, at pixel (x, y) of a frame with geometry g: raw is the frame's
+// WTA map and d2 its right-view keys (both [H][W]).  Every consumer of the LR-checked map
+// computes it on the fly from these two (the median's tiles, the debug stage), so the map itself
+// is never written.
+constexpr uint32_t kD2None = 0xffffffffu;
+__device__ __forceinline__ int lr_at(const Geometry& g, const int16_t* __restrict__ raw,
+                                     const uint32_t* __restrict__ d2, int x, int y, int d12) {
+    const int invalid = (g.minD - 1) * 16;
+    if (x < g.minX1 || x >= g.minX1 + g.W1) return invalid;
+    const size_t ro = (size_t)y * g.W;
+    const int d1 = raw[ro + x];
+    if (d1 == invalid) return d1;
+    const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
+    const int _x = x - _d, x_ = x - d_;
+    if (_x < 0 || _x >= g.W || x_ < 0 || x_ >= g.W) return d1;
+    const uint32_t ka = d2[ro + _x], kb = d2[ro + x_];
+    const int a2 = ka == kD2None ? invalid : (0xffff - (int)(ka & 0xffff)) + g.minX1 - _x;
+    const int b2 = kb == kD2None ? invalid : (0xffff - (int)(kb & 0xffff)) + g.minX1 - x_;
+    const bool bad = a2 >= g.minD && abs(a2 - _d) > d12 && b2 >= g.minD && abs(b2 - d_) > d12;
+    return bad ? invalid : d1;
+}
+// the LR-checked map of F frames (frames fstride apart), materialised (debug stage only)
+void launch_lr_apply(const Geometry& g, const int16_t* raw, const uint32_t* d2, int16_t* out,
                      size_t fstride, int disp12MaxDiff, int F, hipStream_t st);
+// the median's source: A.9 of (raw, d2) per frame (frames fstride apart)
+struct LrSrc {
+    Geometry g;
+    const int16_t* raw;
+    const uint32_t* d2;
+    size_t fstride;
+    int d12;
+};
 
 void launch_fill_s16(int16_t* p, int16_t v, size_t n, hipStream_t st);
+// d2fill (nullable): [F][H][W] right-view keys set to kD2None on the way
 void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t fstride, int W,
-                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split = 1 << 30);
+                      int H, int F, int ftzero, const Planes& pl, hipStream_t st, int split = 1 << 30,
+                      uint32_t* d2fill = nullptr);
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
 void launch_cost_cn3(const Geometry& g, const CostArgs& a, int F, hipStream_t st);  // pl.cn == 3
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);
+// median of the LR-checked map (computed per tile from the WTA map and the right-view keys)
+void launch_median3_lr(const LrSrc& lr, int16_t* dst, int F, hipStream_t st);
 // median of the WTA map with columns outside [c0, c1) read as fill (LR check skipped)
 void launch_median3_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st);
 void launch_mask_cols(const int16_t* src, int16_t* dst, const Geometry& g, int F, hipStream_t st);
-// src may equal dst; out_min (nullable) receives min over each output frame.  median_of
-// (nullable): src is instead the 3x3 median of median_of, computed by the first pass and written
-// to median_out (= src) -- the median filter fused into the labelling
+// src may equal dst; out_min (nullable) receives min over each output frame.  lr (nullable): src
+// is instead the 3x3 median of the LR-checked map, computed by the first pass (which also
+// computes the LR check) and written to median_out (= src) -- A.9 and A.10 fused into the labelling
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
                     int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st,
-                    const int16_t* median_of = nullptr, int16_t* median_out = nullptr);
+                    const LrSrc* lr = nullptr, int16_t* median_out = nullptr);
 void launch_min_s16(const int16_t* img, size_t n_per_frame, size_t fstride, int F, int* out_min,
                     hipStream_t st);
 void launch_reproject_s16(const int16_t* disp, int W, int H, size_t dstride, size_t dfstride,

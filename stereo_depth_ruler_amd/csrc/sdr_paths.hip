@@ -12,8 +12,8 @@
 //
 // k_south_wta: the top-to-bottom chains fused with the winner-take-all (S = sat(sum_r L_r),
 // first minimum, uniqueness, subpixel) as a producer/consumer workgroup; it leaves each pixel's
-// WTA disparity and (minS, bestDisp), and k_lr_check builds the right-view WTA (disp2) of each row
-// in LDS from them and applies the left-right check.
+// WTA disparity and folds its (minS, x) into the right view's WTA keys (disp2) by atomicMin; the
+// left-right check (lr_at) is then computed by the median's tiles from those two maps.
 #include "sdr_device.hpp"
 #include "sdr_internal.hpp"
 
@@ -357,7 +357,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     const double inv100u = 1.0 / (double)(100 - a.uniq) * (1.0 + 0x1p-40);
     const int x = ch.x0;  // matched-range column of this chain
     int16_t* raw = a.disp_raw + (size_t)f * a.disp_fstride + x + g.minX1;
-    uint32_t* keys = a.keys2 + (size_t)f * a.disp_fstride + x;
+    uint32_t* d2 = a.d2 ? a.d2 + (size_t)f * a.disp_fstride : nullptr;
+    const int x2base = x + g.minX1 - g.minD;  // the right-view column of disparity index 0
 
     // window w of staged outputs (rows [w*kStageRows, ...)) to HBM, by the consumer lanes
     auto flush = [&](int w) __attribute__((always_inline)) {
@@ -368,7 +369,11 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
             if (key == kNoWrite) continue;
             const size_t y = (size_t)(ch.y0 + r0 + i);
             raw[y * g.W] = sRaw[w & 1][i];
-            keys[y * g.W] = key;
+            if (d2 && key < kNoWrite) {
+                // A.8's disp2 candidate of this pixel (no return value: a fire-and-forget atomic)
+                const int x2 = x2base - (int)(key & 0xffff);
+                if (x2 >= 0 && x2 < g.W) atomicMin(&d2[y * g.W + x2], (key & 0xffff0000u) | (uint32_t)(0xffff - x));
+            }
         }
     };
 
@@ -481,50 +486,16 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     unroll_rows_tail(consume_sync, b, nblk - 1, std::make_integer_sequence<int, PD>{});
 }
 
-// A.8's right-view WTA (disp2) and A.9, one workgroup per image row: the fused pass's
-// (minS << 16 | bestDisp) per matched pixel is scattered into the row's disp2 keys in LDS by
-// atomicMin on (minS << 16 | 0xffff - x) -- the smallest cost wins, ties to the largest x, as in
-// OpenCV's descending loop with a strict '>' -- then OpenCV's check runs per pixel.
-__global__ __launch_bounds__(256) void k_lr_check(Geometry g0, const int16_t* __restrict__ raw,
-                                                  const uint32_t* __restrict__ keys,
-                                                  int16_t* __restrict__ out, size_t fstride,
-                                                  int disp12MaxDiff) {
+// A.9 materialised (the debug stage of the LR-checked map; the pipeline's median computes it
+// per tile instead)
+__global__ __launch_bounds__(256) void k_lr_apply(Geometry g0, const int16_t* __restrict__ raw,
+                                                  const uint32_t* __restrict__ d2,
+                                                  int16_t* __restrict__ out, size_t fstride, int d12) {
     const Geometry g = frame_geom(g0, blockIdx.y);
-    extern __shared__ uint32_t d2[];  // [W]
     const int y = blockIdx.x, f = blockIdx.y;
-    const size_t ro = (size_t)f * fstride + (size_t)y * g.W;
-    const int invalid = (g.minD - 1) * 16;
-    constexpr uint32_t kNone = 0xffffffffu;
-    for (int x = threadIdx.x; x < g.W; x += 256) d2[x] = kNone;
-    __syncthreads();
-    for (int x = threadIdx.x; x < g.W1; x += 256) {
-        const uint32_t k = keys[ro + x];
-        if (k >= kNoWrite) continue;  // rejected
-        const int x2 = x + g.minX1 - (int)(k & 0xffff) - g.minD;
-        if (x2 >= 0 && x2 < g.W) atomicMin(&d2[x2], (k & 0xffff0000u) | (uint32_t)(0xffff - x));
-    }
-    __syncthreads();
-    auto disp2 = [&](int xx) {
-        const uint32_t k = d2[xx];
-        return k == kNone ? invalid : ((0xffff - (int)(k & 0xffff)) + g.minX1 - xx);
-    };
-    for (int x = threadIdx.x; x < g.W; x += 256) {
-        int d1 = invalid;
-        if (x >= g.minX1 && x < g.minX1 + g.W1) {
-            d1 = raw[ro + x];
-            if (d1 != invalid) {
-                const int _d = d1 >> 4, d_ = (d1 + 15) >> 4;
-                const int _x = x - _d, x_ = x - d_;
-                if (0 <= _x && _x < g.W && 0 <= x_ && x_ < g.W) {
-                    const int a2 = disp2(_x), b2 = disp2(x_);
-                    if (a2 >= g.minD && abs(a2 - _d) > disp12MaxDiff && b2 >= g.minD &&
-                        abs(b2 - d_) > disp12MaxDiff)
-                        d1 = invalid;
-                }
-            }
-        }
-        out[ro + x] = (int16_t)d1;
-    }
+    const size_t fo = (size_t)f * fstride;
+    for (int x = threadIdx.x; x < g.W; x += 256)
+        out[fo + (size_t)y * g.W + x] = (int16_t)lr_at(g, raw + fo, d2 + fo, x, y, d12);
 }
 
 template <int DPL, bool PAD>
@@ -552,10 +523,9 @@ void launch_south_wta(const Geometry& g, const PathLaunch& pl, const SouthWtaArg
     }
 }
 
-void launch_lr_check(const Geometry& g, const int16_t* raw, const uint32_t* keys, int16_t* out,
+void launch_lr_apply(const Geometry& g, const int16_t* raw, const uint32_t* d2, int16_t* out,
                      size_t fstride, int disp12MaxDiff, int F, hipStream_t st) {
-    hipLaunchKernelGGL(k_lr_check, dim3(g.H, F), dim3(256), (size_t)g.W * 4, st, g, raw, keys, out,
-                       fstride, disp12MaxDiff);
+    hipLaunchKernelGGL(k_lr_apply, dim3(g.H, F), dim3(256), 0, st, g, raw, d2, out, fstride, disp12MaxDiff);
 }
 
 }  // namespace sdr

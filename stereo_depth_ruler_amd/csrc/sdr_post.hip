@@ -50,6 +50,54 @@ void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipSt
     hipLaunchKernelGGL(k_median3, grid, dim3(256), 0, st, src, dst, W, H);
 }
 
+// the (TW + 2) x (TH + 2) neighbourhood of a TW x TH tile of the LR-checked map (A.9 from the WTA
+// map and the right-view keys), rows and columns clamped (medianBlur's BORDER_REPLICATE), in LDS
+template <int TW, int TH>
+__device__ __forceinline__ void stage_lr_halo(const LrSrc& lr, int tx0, int ty0, int f, int16_t* hal) {
+    const Geometry g = frame_geom(lr.g, f);
+    const size_t fo = (size_t)f * lr.fstride;
+    constexpr int HW = TW + 2, N = HW * (TH + 2);
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+        const int hy = i / HW, hx = i - hy * HW;
+        const int y = min(max(ty0 - 1 + hy, 0), g.H - 1), x = min(max(tx0 - 1 + hx, 0), g.W - 1);
+        hal[i] = (int16_t)lr_at(g, lr.raw + fo, lr.d2 + fo, x, y, lr.d12);
+    }
+}
+
+// 3x3 median at (lx, ly) of a tile from its staged neighbourhood (row pitch HW)
+template <int HW>
+__device__ __forceinline__ int median3_lds(const int16_t* hal, int lx, int ly) {
+    int p[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) p[i * 3 + j] = hal[(ly + i) * HW + lx + j];
+#define SDR_S(a, b) { int t_ = min(p[a], p[b]); p[b] = max(p[a], p[b]); p[a] = t_; }
+    SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 1) SDR_S(3, 4) SDR_S(6, 7)
+    SDR_S(1, 2) SDR_S(4, 5) SDR_S(7, 8) SDR_S(0, 3) SDR_S(5, 8) SDR_S(4, 7)
+    SDR_S(3, 6) SDR_S(1, 4) SDR_S(2, 5) SDR_S(4, 7) SDR_S(4, 2) SDR_S(6, 4)
+    SDR_S(4, 2)
+#undef SDR_S
+    return p[4];
+}
+
+// A.9 + A.10 without the speckle filter: 64 x 4 tiles, the LR check computed once per staged pixel
+__global__ __launch_bounds__(256) void k_median3_lr(LrSrc lr, int16_t* __restrict__ dst) {
+    __shared__ int16_t hal[66 * 6];
+    const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 4, f = blockIdx.z;
+    stage_lr_halo<64, 4>(lr, tx0, ty0, f, hal);
+    __syncthreads();
+    const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+    const int x = tx0 + lx, y = ty0 + ly;
+    if (x >= lr.g.W || y >= lr.g.H) return;
+    dst[(size_t)f * lr.g.W * lr.g.H + (size_t)y * lr.g.W + x] = (int16_t)median3_lds<66>(hal, lx, ly);
+}
+
+void launch_median3_lr(const LrSrc& lr, int16_t* dst, int F, hipStream_t st) {
+    dim3 grid((lr.g.W + 63) / 64, (lr.g.H + 3) / 4, F);
+    hipLaunchKernelGGL(k_median3_lr, grid, dim3(256), 0, st, lr, dst);
+}
+
 // the column mask of frame f: the matched columns [minX1, minX1 + W1) and INVALID of its matcher
 __global__ __launch_bounds__(256) void k_median3_cols(const int16_t* __restrict__ src,
                                                       int16_t* __restrict__ dst, Geometry g) {
@@ -165,28 +213,35 @@ __device__ __forceinline__ bool joined(int a, int b, int newVal, int maxDiff) {
 }
 
 // 256 threads = 4 waves; pixel i = t + 256k (k < 4): a wave covers two tile rows per k.
-// MED: img is the median filter's input; the tile's medians are computed here and written to
-// med (the image merge and apply read), which saves the median pass.
-template <bool MED>
+// LRMED: the image is the 3x3 median of the LR-checked map; the tile's neighbourhood of that map
+// is computed into LDS (A.9 from the WTA map and the right-view keys), its medians are computed
+// here and written to med (the image merge and apply read): the LR check and the median pass
+// run inside the labelling's first pass.
+template <bool LRMED>
 __global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ img, int16_t* __restrict__ med,
                                                    int* __restrict__ P, int* __restrict__ S, int W, int H,
-                                                   int newVal, int maxDiff, int* out_min) {
+                                                   int newVal, int maxDiff, int* out_min, LrSrc lr) {
     __shared__ int v[kCT * kCT];
     __shared__ int lab[kCT * kCT];
     __shared__ int cnt[kCT * kCT];
+    __shared__ int16_t hal[LRMED ? (kCT + 2) * (kCT + 2) : 1];
     const int tx0 = blockIdx.x * kCT, ty0 = blockIdx.y * kCT;
     const size_t fo = (size_t)blockIdx.z * W * H;
     const int t = threadIdx.x, lane = t & 63, lx = t & (kCT - 1);
     if (out_min && t < kMinSlots && blockIdx.x == 0 && blockIdx.y == 0) out_min[blockIdx.z * kMinSlots + t] = 32767;
     const int gx = tx0 + lx;
+    if (LRMED) {
+        stage_lr_halo<kCT, kCT>(lr, tx0, ty0, blockIdx.z, hal);
+        __syncthreads();
+    }
     int val[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int i = t + 256 * k, gy = ty0 + (i >> 5);
-        if (MED) {
+        if (LRMED) {
             val[k] = newVal;
             if (gx < W && gy < H) {
-                val[k] = median3_at(img + fo, W, H, gx, gy);
+                val[k] = median3_lds<kCT + 2>(hal, lx, i >> 5);
                 med[fo + (size_t)gy * W + gx] = (int16_t)val[k];
             }
         } else {
@@ -354,15 +409,15 @@ __global__ __launch_bounds__(256) void k_ccl_apply(const int16_t* src, int16_t* 
 
 void launch_speckle(const int16_t* src, int16_t* dst, int W, int H, int F, int newVal, int maxSize,
                     int maxDiff, int* labels, int* sizes, int* out_min, hipStream_t st,
-                    const int16_t* median_of, int16_t* median_out) {
+                    const LrSrc* lr, int16_t* median_out) {
     const int n = W * H;
     const dim3 tiles((W + kCT - 1) / kCT, (H + kCT - 1) / kCT, F);
-    if (median_of)
-        hipLaunchKernelGGL((k_ccl_local<true>), tiles, dim3(256), 0, st, median_of, median_out, labels, sizes, W,
-                           H, newVal, maxDiff, out_min);
+    if (lr)
+        hipLaunchKernelGGL((k_ccl_local<true>), tiles, dim3(256), 0, st, (const int16_t*)nullptr, median_out,
+                           labels, sizes, W, H, newVal, maxDiff, out_min, *lr);
     else
         hipLaunchKernelGGL((k_ccl_local<false>), tiles, dim3(256), 0, st, src, (int16_t*)nullptr, labels, sizes,
-                           W, H, newVal, maxDiff, out_min);
+                           W, H, newVal, maxDiff, out_min, LrSrc{});
     const int nb = ((W - 1) / kCT) * H + ((H - 1) / kCT) * W;
     if (nb > 0)
         hipLaunchKernelGGL(k_ccl_merge, dim3((unsigned)min((nb + 255) / 256, 1024), F), dim3(256), 0,

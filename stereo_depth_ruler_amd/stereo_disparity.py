@@ -23,9 +23,14 @@ from .ximgproc import createDisparityWLSFilter
 
 
 class StereoDisparity:
-    # show_depthMap's `static double zmin_smooth = 1000.0, zmax_smooth = 2000.0` (one per process)
+    # show_depthMap's `static double zmin_smooth = 1000.0, zmax_smooth = 2000.0` (one per process).
+    # One state: it lives where the last call ran (the host array, or a float64 tensor on that
+    # call's device) and moves with the first call of the other kind, so a process mixing numpy
+    # and device inputs smooths one range as the reference does, and device-only callers stay
+    # asynchronous.
     _zrange_host = np.array([1000.0, 2000.0])
     _zrange_dev = {}
+    _zrange_owner = None  # None: _zrange_host is current; else the device index holding it
 
     def __init__(self, Q_matrix, device: int = 0):
         self._device = int(device)
@@ -81,11 +86,19 @@ class StereoDisparity:
 
     def show_depthMap(self, depth):
         """stereo_disparity.cpp:83-124 on computeDepth's output (or a Z map)."""
+        cls = StereoDisparity
         if _is_cuda(depth):
             dev = depth.device.index
-            z = StereoDisparity._zrange_dev.get(dev)
+            z = cls._zrange_dev.get(dev)
             if z is None:
-                z = torch.tensor([1000.0, 2000.0], dtype=torch.float64, device=depth.device)
-                StereoDisparity._zrange_dev[dev] = z
+                z = torch.empty(2, dtype=torch.float64, device=depth.device)
+                cls._zrange_dev[dev] = z
+            if cls._zrange_owner != dev:
+                src = cls._zrange_host if cls._zrange_owner is None else cls._zrange_dev[cls._zrange_owner].cpu().numpy()
+                z.copy_(torch.from_numpy(np.array(src, dtype=np.float64)))
+                cls._zrange_owner = dev
             return self._disp().show_depth_map(depth, zrange=z)
-        return self._disp().show_depth_map(depth, zrange=StereoDisparity._zrange_host)
+        if cls._zrange_owner is not None:
+            cls._zrange_host[:] = cls._zrange_dev[cls._zrange_owner].cpu().numpy()
+            cls._zrange_owner = None
+        return self._disp().show_depth_map(depth, zrange=cls._zrange_host)

@@ -70,6 +70,11 @@ def test_scratch_bytes_is_pure_host():
     assert n >= 2 * cells * 2  # cost volume + path sums, int16
     bad = _lib.SgbmParams(0, 100, 5, 600, 2400, 1, 63, 12, 200, 2, 0, 4, 0)
     assert _lib.lib().sdr_sgbm_scratch_bytes(ctypes.byref(bad), 1280, 720, 1) == 0
+    # colour input: three operand sets per image (the L pack and the R pair planes, 36 B/px/channel)
+    n3 = _lib.lib().sdr_sgbm_scratch_bytes_cn(ctypes.byref(p), 1280, 720, 3, 1)
+    assert n3 - n == 2 * 36 * 1280 * 720
+    assert _lib.lib().sdr_sgbm_scratch_bytes_cn(ctypes.byref(p), 1280, 720, 1, 1) == n
+    assert _lib.lib().sdr_sgbm_scratch_bytes_cn(ctypes.byref(p), 1280, 720, 2, 1) == 0
 
 
 def test_create_without_gpu_fails_loudly():

@@ -1,23 +1,24 @@
 // sdr_cost3.hip -- the cost-volume kernel for 3-channel input (calcPixelCostBT's cn == 3 branch:
 // each channel's Sobel and raw BT costs are summed into the pixel cost).  The kernel template is
-// sdr_cost_kernel.hpp; this file holds its CN = 3 instantiations.
+// sdr_cost_kernel.hpp; this file holds its CN = 3 instantiations for D <= 128 (K = 1) and the
+// dispatch; sdr_cost3k2.hip the D > 128 ones (two translation units that compile in parallel).
 #include "sdr_cost_kernel.hpp"
 
 namespace sdr {
 
+void launch_cost_cn3_k2(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
+
 void launch_cost_cn3(const Geometry& g, const CostArgs& a, int F, hipStream_t st) {
-    const int NR = 2 * g.SH2 + 1;
-    const bool k2 = g.D > 128;
-#define SDR_COST(NRV)                                                 \
-    case NRV:                                                         \
-        if (k2) launch_cost_t<NRV, 2, 3>(g, a, F, st);                \
-        else launch_cost_t<NRV, 1, 3>(g, a, F, st);                   \
-        break;
-    switch (NR) {
-        SDR_COST(1) SDR_COST(3) SDR_COST(5) SDR_COST(7) SDR_COST(9) SDR_COST(11)
+    if (g.D > 128) return launch_cost_cn3_k2(g, a, F, st);
+    switch (2 * g.SH2 + 1) {
+        case 1: launch_cost_t<1, 1, 3>(g, a, F, st); break;
+        case 3: launch_cost_t<3, 1, 3>(g, a, F, st); break;
+        case 5: launch_cost_t<5, 1, 3>(g, a, F, st); break;
+        case 7: launch_cost_t<7, 1, 3>(g, a, F, st); break;
+        case 9: launch_cost_t<9, 1, 3>(g, a, F, st); break;
+        case 11: launch_cost_t<11, 1, 3>(g, a, F, st); break;
         default: break;
     }
-#undef SDR_COST
 }
 
 }  // namespace sdr

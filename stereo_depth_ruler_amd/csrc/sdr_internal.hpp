@@ -11,8 +11,10 @@
 namespace sdr {
 
 // partial per-frame minima of the int16 disparity (launch_min_s16 / launch_speckle's out_min):
-// [F][kMinSlots] ints, consumed by launch_reproject_s16
-constexpr int kMinSlots = 32;
+// [F][kMinSlots] ints, consumed by launch_reproject_s16 (wave-uniform scalar loads).  Block b
+// folds into slot b % kMinSlots: 2048 apply blocks make 8 same-address atomics per slot (32
+// slots: 64, which serialised to ~13 us of the apply pass)
+constexpr int kMinSlots = 256;
 
 
 // Device buffer that only grows (engine and WLS scratch); ensure() returns an SDR_* status.

@@ -52,15 +52,51 @@ void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipSt
 
 // the (TW + 2) x (TH + 2) neighbourhood of a TW x TH tile of the LR-checked map (A.9 from the WTA
 // map and the right-view keys), rows and columns clamped (medianBlur's BORDER_REPLICATE), in LDS
-template <int TW, int TH>
+// (lr_at unrolled over a thread's NPT pixels: all WTA loads, then all key loads, so the block
+// pays two dependent memory round trips, not two per pixel)
+template <int TW, int TH, int NT>
 __device__ __forceinline__ void stage_lr_halo(const LrSrc& lr, int tx0, int ty0, int f, int16_t* hal) {
     const Geometry g = frame_geom(lr.g, f);
     const size_t fo = (size_t)f * lr.fstride;
-    constexpr int HW = TW + 2, N = HW * (TH + 2);
-    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const int16_t* raw = lr.raw + fo;
+    const uint32_t* d2 = lr.d2 + fo;
+    constexpr int HW = TW + 2, N = HW * (TH + 2), NPT = (N + NT - 1) / NT;
+    const int invalid = (g.minD - 1) * 16, c0 = g.minX1, c1 = g.minX1 + g.W1;
+    int d1[NPT], xa[NPT], xb[NPT];
+    size_t ro[NPT];
+    bool m[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = min((int)threadIdx.x + k * NT, N - 1);
         const int hy = i / HW, hx = i - hy * HW;
         const int y = min(max(ty0 - 1 + hy, 0), g.H - 1), x = min(max(tx0 - 1 + hx, 0), g.W - 1);
-        hal[i] = (int16_t)lr_at(g, lr.raw + fo, lr.d2 + fo, x, y, lr.d12);
+        ro[k] = (size_t)y * g.W;
+        m[k] = x >= c0 && x < c1;
+        d1[k] = raw[ro[k] + min(max(x, c0), c1 - 1)];  // matched columns only hold values
+        xa[k] = x;
+    }
+    uint32_t ka[NPT], kb[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        if (!m[k]) d1[k] = invalid;
+        const int x = xa[k];
+        xa[k] = x - (d1[k] >> 4);
+        xb[k] = x - ((d1[k] + 15) >> 4);
+        ka[k] = d2[ro[k] + min(max(xa[k], 0), g.W - 1)];
+        kb[k] = d2[ro[k] + min(max(xb[k], 0), g.W - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; k++) {
+        const int i = threadIdx.x + k * NT;
+        if (i >= N) break;
+        int v = d1[k];
+        const int _d = v >> 4, d_ = (v + 15) >> 4;
+        if (v != invalid && xa[k] >= 0 && xa[k] < g.W && xb[k] >= 0 && xb[k] < g.W) {
+            const int a2 = ka[k] == kD2None ? invalid : (0xffff - (int)(ka[k] & 0xffff)) + g.minX1 - xa[k];
+            const int b2 = kb[k] == kD2None ? invalid : (0xffff - (int)(kb[k] & 0xffff)) + g.minX1 - xb[k];
+            if (a2 >= g.minD && abs(a2 - _d) > lr.d12 && b2 >= g.minD && abs(b2 - d_) > lr.d12) v = invalid;
+        }
+        hal[i] = (int16_t)v;
     }
 }
 
@@ -85,7 +121,7 @@ __device__ __forceinline__ int median3_lds(const int16_t* hal, int lx, int ly) {
 __global__ __launch_bounds__(256) void k_median3_lr(LrSrc lr, int16_t* __restrict__ dst) {
     __shared__ int16_t hal[66 * 6];
     const int tx0 = blockIdx.x * 64, ty0 = blockIdx.y * 4, f = blockIdx.z;
-    stage_lr_halo<64, 4>(lr, tx0, ty0, f, hal);
+    stage_lr_halo<64, 4, 256>(lr, tx0, ty0, f, hal);
     __syncthreads();
     const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
     const int x = tx0 + lx, y = ty0 + ly;
@@ -228,10 +264,11 @@ __global__ __launch_bounds__(256) void k_ccl_local(const int16_t* __restrict__ i
     const int tx0 = blockIdx.x * kCT, ty0 = blockIdx.y * kCT;
     const size_t fo = (size_t)blockIdx.z * W * H;
     const int t = threadIdx.x, lane = t & 63, lx = t & (kCT - 1);
-    if (out_min && t < kMinSlots && blockIdx.x == 0 && blockIdx.y == 0) out_min[blockIdx.z * kMinSlots + t] = 32767;
+    if (out_min && blockIdx.x == 0 && blockIdx.y == 0)
+        for (int j = t; j < kMinSlots; j += 256) out_min[blockIdx.z * kMinSlots + j] = 32767;
     const int gx = tx0 + lx;
     if (LRMED) {
-        stage_lr_halo<kCT, kCT>(lr, tx0, ty0, blockIdx.z, hal);
+        stage_lr_halo<kCT, kCT, 256>(lr, tx0, ty0, blockIdx.z, hal);
         __syncthreads();
     }
     int val[4];
@@ -332,15 +369,26 @@ __global__ __launch_bounds__(256) void k_ccl_merge(const int16_t* __restrict__ i
             step = 1;
             inner = (x % kCT) != 0;
         }
-        const int va = I[a], vb = I[b];
+        // every load this pair may need is issued up front (the previous pair's values, and the
+        // labels of a and b with one more hop): three dependent round trips instead of up to six
+        const int sa = inner ? a - step : a, sb = inner ? b - step : b;
+        const int va = I[a], vb = I[b], pa = I[sa], pb = I[sb];
+        const int ra = uf_load(Pf, a), rb = uf_load(Pf, b);
         if (!joined(va, vb, newVal, maxDiff)) continue;
-        if (inner) {
-            const int pa = I[a - step], pb = I[b - step];
-            if (joined(pa, pb, newVal, maxDiff) && joined(va, pa, newVal, maxDiff) &&
-                joined(vb, pb, newVal, maxDiff))
-                continue;
+        if (inner && joined(pa, pb, newVal, maxDiff) && joined(va, pa, newVal, maxDiff) &&
+            joined(vb, pb, newVal, maxDiff))
+            continue;
+        int x = uf_load(Pf, ra), y = uf_load(Pf, rb);
+        if (x == ra && y == rb) {
+            // both were roots: link the larger under the smaller (uf_unite's step without its finds)
+            if (x == y) continue;
+            const int lo = min(x, y), hi = max(x, y);
+            const int old = atomicMin(&Pf[hi], lo);
+            if (old == hi) continue;
+            x = lo;
+            y = old;
         }
-        uf_unite(Pf, a, b);
+        uf_unite(Pf, x, y);
     }
 }
 
@@ -474,16 +522,21 @@ __global__ __launch_bounds__(256) void k_reproject_s16(const int16_t* disp, int 
                                                        int hm, const int* mins, float* xyz,
                                                        size_t xstride, size_t xfstride) {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    double mind = (double)FLT_MAX;
+    if (hm) {
+        // the frame minimum from its slots: kMinSlots / 64 coalesced loads per lane + a wave minimum
+        // (before any lane leaves)
+        static_assert(kMinSlots % 64 == 0, "slots per lane");
+        const int lane = threadIdx.x & 63;
+        int m = 32767;
+#pragma unroll
+        for (int k = 0; k < kMinSlots / 64; k++) m = min(m, mins[f * kMinSlots + k * 64 + lane]);
+        m = (int)wave_min_u32_uniform((uint32_t)(m + 32768)) - 32768;
+        mind = (double)((float)m * 0.0625f);
+    }
     if (x >= W) return;
     const int v = disp[(size_t)f * dfstride + (size_t)y * dstride + x];
     const double d = (double)((float)v * 0.0625f);
-    double mind = (double)FLT_MAX;
-    if (hm) {
-        int m = mins[f * kMinSlots];  // wave-uniform: scalar loads
-#pragma unroll
-        for (int k = 1; k < kMinSlots; k++) m = min(m, mins[f * kMinSlots + k]);
-        mind = (double)((float)m * 0.0625f);
-    }
     reproject_px(Q, x, y, d, mind, hm, xyz + (size_t)f * xfstride + (size_t)y * xstride + 3 * (size_t)x);
 }
 

@@ -321,6 +321,10 @@ struct sdr_sgbm {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hxyz, keys2;
+    // MODE_HH row sweeps: [2 passes][slots][tiles][2] counters, the error word, the edge rings;
+    // sweep_err_host: the error word of the last sweep, copied back asynchronously (page-locked)
+    Buf sweep;
+    int* sweep_err_host = nullptr;
     HostXfer hx;  // pinned staging of the host-pointer entry points
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
@@ -382,6 +386,17 @@ struct KTimer {
 
 
 static int npaths_of(int mode);
+// batches from this many frames run MODE_HH's N/NE/NW and SE/SW as row sweeps (k_sweep): a sweep
+// walks a frame's rows in order, so it pays one cross-tile hand-over per row per frame and only
+// amortises that latency over several frames in flight
+constexpr int kSweepMinFrames = 8;
+
+// A sweep's workgroups wait on each other, so its grid must become resident as a whole: other
+// kernels only delay that (they finish without waiting on anything), but two sweeps in flight at
+// once could each hold part of the chip while waiting for the rest.  Sweeps of every handle and
+// stream of a device are therefore chained in submission order through one event per device.
+static std::mutex g_sweep_mu;
+static std::map<int, hipEvent_t> g_sweep_last;
 
 static size_t scratch_bytes(const Eff& e, int F, std::vector<Stripe>* st, int cn) {
     const sdr::Geometry& g = e.g;
@@ -451,8 +466,20 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     if ((rc = check_frame(e))) return rc;
 
+    // a failed neighbour wait of an earlier call's MODE_HH sweep (its error word, copied back
+    // after that launch) is reported now: the frames it produced were wrong
+    if (h->sweep_err_host && __atomic_exchange_n(h->sweep_err_host, 0, __ATOMIC_RELAXED))
+        return fail(SDR_ERR_DEVICE, "a MODE_HH row sweep of an earlier call timed out waiting for a tile");
     const size_t cells = (size_t)H * g.W1 * g.D;
     const int P = npaths_of(e.mode);
+    // batched MODE_HH: N/NE/NW and SE/SW as two row-synchronous sweeps into one record each
+    // (when every tile of the frames in flight fits the resident grid); the records are then
+    // E, W, up, down -- saturated sums of non-negative path costs, so the grouping is exact
+    sdr::SweepShape shp[2] = {};  // [0]: down (SE, SW), [1]: up (N, NE, NW)
+    if (e.mode == SDR_MODE_HH && F >= kSweepMinFrames && g.W1 > 0)
+        for (int up = 0; up < 2; up++) shp[up] = sdr::sweep_shape(g, F, up != 0);
+    const bool sweep = shp[0].nslots > 0 && shp[1].nslots > 0;
+    const int nrec = sweep ? 4 : P - 1;  // L records per pixel
     std::vector<Stripe> stripes;
     if (e.mode == SDR_MODE_SGBM_3WAY) stripes_of(e, &stripes);
     if (stripes.size() + 2 > (size_t)sdr::kMaxPathDirs) return fail(SDR_ERR_ARG, "too many 3WAY stripes");
@@ -465,8 +492,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     if ((rc = ensure(h->sink, sdr::cost_sink_bytes(g)))) return rc;
     // the path kernels' loads overrun a chain's ends by up to kSouthPad rows: slack both sides
     const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
-    const size_t lslack = slack * (P - 1);
-    const size_t lfs = (size_t)(P - 1) * cells;  // L elements per frame, [H][W1][P-1][D]
+    const size_t lslack = slack * nrec;
+    const size_t lfs = (size_t)nrec * cells;  // L elements per frame, [H][W1][nrec][D]
     if ((rc = ensure(h->C, (F * cells + 2 * slack) * 2))) return rc;
     if ((rc = ensure(h->Lr, (F * lfs + 2 * lslack) * 2))) return rc;
     if ((rc = ensure(h->keys2, F * px * 4))) return rc;
@@ -483,7 +510,21 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     h->path_lslack = lslack;
     int16_t* C = (int16_t*)h->C.p + slack;
     int16_t* Caux = (int16_t*)h->Caux.p;
-    int16_t* Lr = (int16_t*)h->Lr.p + lslack;  // [F][H][W1][P-1][D]
+    int16_t* Lr = (int16_t*)h->Lr.p + lslack;  // [F][H][W1][nrec][D]
+    // [pass][slots][tiles][2] counters, the error word, then the edge ring (sized for either pass)
+    size_t flags_n[2] = {0, 0}, edge_bytes = 0;
+    for (int up = 0; up < 2; up++) {
+        flags_n[up] = (size_t)shp[up].nslots * shp[up].ntiles * 2;
+        edge_bytes = std::max(edge_bytes, (size_t)shp[up].nslots * shp[up].ntiles * 4 * shp[up].cols * g.D * 2);
+    }
+    const size_t sweep_flags = (flags_n[0] + flags_n[1]) * sizeof(int);
+    if (sweep) {
+        if ((rc = ensure(h->sweep, sweep_flags + 256 + edge_bytes))) return rc;
+        if (!h->sweep_err_host && hipHostMalloc((void**)&h->sweep_err_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+            h->sweep_err_host = nullptr;
+            return fail(SDR_ERR_NOMEM, "hipHostMalloc failed");
+        }
+    }
     int16_t* draw = (int16_t*)h->draw.p;
 
     sdr::Planes pl;
@@ -541,7 +582,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     pls.C = plS.C = C;
     pls.cs_fstride = plS.cs_fstride = cells;
     pls.l_fstride = plS.l_fstride = lfs;
-    pls.l_pix = plS.l_pix = (P - 1) * g.D;
+    pls.l_pix = plS.l_pix = nrec * g.D;
     pls.aux_fstride = plS.aux_fstride = aux_fstride;
     int nbuf = 0;
     auto add_dir = [&](sdr::PathLaunch& pl, int dir, int nch, int16_t* out) {
@@ -577,6 +618,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         // computeDisparitySGBM_HH4: the two vertical and the two horizontal directions
         add_dir(plS, sdr::DIR_S, nS, nullptr);
         add_dir(pls, sdr::DIR_N, nS, buf());
+    } else if (sweep) {
+        add_dir(plS, sdr::DIR_S, nS, nullptr);  // records 2 and 3: the up and down sweeps
     } else {
         add_dir(plS, sdr::DIR_S, nS, nullptr);
         if (e.mode == SDR_MODE_HH) add_dir(pls, sdr::DIR_N, nS, buf());
@@ -592,11 +635,38 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         for (int i = 0; i < pl->ndirs; i++) pl->prefix[i + 1] = pl->prefix[i] + pl->d[i].nchains;
     }
     { KTimer kt(h, SDR_KERNEL_PATHS); sdr::launch_paths(g, pls, F, st); }
+    if (sweep) {
+        KTimer kt(h, SDR_KERNEL_PATHS);
+        char* sb = (char*)h->sweep.p;
+        SDR_HIP(hipMemsetAsync(sb, 0, sweep_flags + sizeof(int), st));
+        sdr::SweepArgs sa{};
+        sa.C = C;
+        sa.cs_fstride = cells;
+        sa.l_fstride = lfs;
+        sa.l_pix = nrec * g.D;
+        sa.flags = (int*)sb;
+        sa.err = (int*)(sb + sweep_flags);
+        sa.edge = (uint32_t*)(sb + sweep_flags + 256);
+        std::lock_guard<std::mutex> lk(g_sweep_mu);
+        hipEvent_t& last = g_sweep_last[h->device];
+        if (last) SDR_HIP(hipStreamWaitEvent(st, last, 0));
+        else SDR_HIP(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+        for (int up = 1; up >= 0; up--) {
+            sa.up = up;
+            sa.ntiles = shp[up].ntiles;
+            sa.nslots = shp[up].nslots;
+            sa.rec = Lr + (size_t)(up ? 2 : 3) * g.D;
+            sdr::launch_sweep(g, sa, F, st);
+            sa.flags += flags_n[up];
+        }
+        SDR_HIP(hipEventRecord(last, st));
+        SDR_HIP(hipMemcpyAsync(h->sweep_err_host, sb + sweep_flags, sizeof(int), hipMemcpyDeviceToHost, st));
+    }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
     sdr::SouthWtaArgs wa{};
     wa.L = Lr;
-    wa.npaths = P;
+    wa.npaths = nrec + 1;
     wa.disp_raw = draw;
     wa.d2 = d2;
     wa.disp_fstride = px;
@@ -688,7 +758,8 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (Buf* b : {&h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
+    if (h->sweep_err_host) (void)hipHostFree(h->sweep_err_host);
+    for (Buf* b : {&h->sweep, &h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})

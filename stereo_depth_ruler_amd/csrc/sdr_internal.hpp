@@ -124,6 +124,39 @@ struct PathLaunch {
     PathDir d[kMaxPathDirs];
 };
 
+// Row-synchronous sweeps of batched MODE_HH (sdr_paths.hip, k_sweep): the upward directions N, NE
+// and NW (up = 1) or the downward diagonals SE and SW (up = 0) of a frame in one pass over its
+// rows, column tiles of kSweepTile columns per workgroup handing the diagonals' tile-edge path
+// costs to their neighbours each row.  Each pass reads a cost row once for all its directions
+// and writes their saturated sum as one record slot.
+constexpr int kSweepOwn = 10;                     // waves holding the tile's own columns
+constexpr int kSweepWaves = kSweepOwn + 2;        // + one halo wave on each side
+// columns per wave: 8, or 6 for the three-direction pass at D > 128 (its 48 path-cost words per
+// lane and column must fit 3 waves per SIMD without spilling); tile = kSweepOwn waves of them.
+// A halo reload every cols - 1 rows: a halo column j (counted from the tile's far side) goes wrong
+// j rows after a reload, and the tile's first column takes the halo's nearest one from the row
+// before through LDS, which the halo wave computed before the reload
+__host__ __device__ constexpr int sweep_cols(int dpl, bool up) { return dpl == 4 && up ? 6 : 8; }
+struct SweepArgs {
+    const int16_t* C;
+    size_t cs_fstride;     // elements per frame of C
+    int16_t* rec;          // this pass's record slot (L records + slot * D)
+    size_t l_fstride;      // elements per frame of the records
+    int l_pix;             // elements per pixel record
+    uint32_t* edge;        // [nslots][ntiles][2 sides][2][cols][D/2] boundary columns' path costs
+    int* flags;            // [nslots][ntiles][2 sides] rows published (zero before the launch)
+    int* err;              // set when a neighbour wait times out (never, with every tile resident)
+    int ntiles, nslots;    // frames in flight = nslots (workgroups = nslots * ntiles, all resident)
+    int up;
+};
+// a pass's tiling: columns per wave, tiles per frame, frames in flight (slots; 0: the frame's
+// tiles do not fit the resident grid)
+struct SweepShape {
+    int cols, ntiles, nslots;
+};
+SweepShape sweep_shape(const Geometry& g, int F, bool up);
+void launch_sweep(const Geometry& g, const SweepArgs& a, int F, hipStream_t st);
+
 // top-to-bottom direction fused with the WTA (sdr_paths.hip): the other P-1 directions' L in
 // sum order with the fused direction at position kSouthIdx
 constexpr int kSouthIdx = 2;  // summation order E, W, S, SE, SW, N, NE, NW

@@ -1,0 +1,55 @@
+"""Batched MODE_HH through the row-synchronous sweeps (k_sweep: N/NE/NW up, SE/SW down, one
+record each) against the oracle, frame by frame.  Batches of >= 8 frames take the sweep path;
+single frames take k_paths' per-direction chains, so the two formulations are also compared with
+each other.  Shapes cover one tile and partial last tiles (kSweepTile = 32 columns), padded
+disparity lanes (D < 64 * DPL at both lane widths) and the int16 extremes (binary / noise pairs:
+saturated sums)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import stereo_depth_ruler_amd as sdr  # noqa: E402
+from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+
+
+def _batch(kind, F, H, W, D, seed):
+    Ls = np.empty((F, H, W), np.uint8)
+    Rs = np.empty((F, H, W), np.uint8)
+    for i in range(F):
+        if kind == "textured":
+            Ls[i], Rs[i], _ = S.make_pair(H, W, D, seed + i)
+        else:
+            Ls[i], Rs[i] = S.adversarial_pair(kind, H, W, D, seed=seed + i)
+    return Ls, Rs
+
+
+@pytest.mark.parametrize("kind,F,H,W,D,speckle,seed", [
+    ("textured", 8, 40, 200, 64, 30, 1),    # 5 tiles, the last partial (W1 = 136)
+    ("textured", 9, 33, 90, 48, 0, 2),      # one tile + 10 columns, D padded (DPL 2)
+    ("noise", 8, 24, 60, 32, 0, 3),         # W1 = 28: a single partial tile
+    ("binary", 8, 30, 120, 16, 0, 4),       # saturated S sums
+    ("textured", 8, 26, 260, 160, 20, 5),   # DPL 4 with padded lanes
+    ("steps", 10, 20, 100, 32, 0, 6),
+])
+def test_hh_sweep_batch_bit_exact(oracle, kind, F, H, W, D, speckle, seed):
+    args = (0, D, 5, 600, 2400, 1, 63, 10, speckle, 2, sdr.MODE_HH)
+    Ls, Rs = _batch(kind, F, H, W, D, seed)
+    dev = torch.device("cuda", 0)
+    m = sdr.StereoSGBM.create(*args)
+    out = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    for i in range(F):
+        ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
+        assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
+    # the same frames one at a time (k_paths' chains) and again as a batch on the same handle
+    # (the sweep's counters and edge rings start over every call)
+    for i in (0, F - 1):
+        assert np.array_equal(m.compute(Ls[i], Rs[i]), out[i])
+    again = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    assert np.array_equal(again, out)
+    m.close()

@@ -234,7 +234,7 @@ def main():
     KERNEL_KINDS = {"prefilter": _sg.KERNEL_PREFILTER, "k_cost": _sg.KERNEL_COST, "k_paths": _sg.KERNEL_PATHS,
                     "k_south_wta": _sg.KERNEL_WTA_LR, "k_lr_check": _sg.KERNEL_LR_CHECK,
                     "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
-                    "reproject": _sg.KERNEL_REPROJECT}
+                    "reproject": _sg.KERNEL_REPROJECT, "k_sweep": _sg.KERNEL_SWEEP}
 
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
     D, mode = args[1], args[10]
@@ -384,33 +384,52 @@ def main():
         kern = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
                        "share": round(ms / all_ms, 4) if all_ms else None}
                 for name, (ms, c) in per_kind.items() if c}
-        tot_ms, cnt = per_kind["k_paths"]
         frames_seen = per_kind["prefilter"][1]
-        if not cnt:
+        if not per_kind["k_paths"][1]:
             return kern, None
-        # k_paths runs every direction except top-to-bottom (that one is fused into k_south_wta):
-        # each of its P-1 directions reads C (2 B/cell) and writes its own L_r (2 B/cell)
-        bytes_per_launch = cells * 4 * (P - 1)
+        # algorithmic bytes per launch of the three path kernels (2 B per int16 cell):
+        #   k_paths: each of its directions reads C and writes its own record;
+        #   k_sweep (batched MODE_HH): one pass reads C once and writes one record for its
+        #     directions (up: N, NE, NW; down: SE, SW), so k_paths keeps E and W only;
+        #   k_south_wta: reads C and the other directions' records (top-to-bottom fused)
+        sweep = per_kind["k_sweep"][1] > 0
+        kp_dirs = 2 if sweep else P - 1
+        nrec = 4 if sweep else P - 1
+        models = {
+            "k_paths": (cells * 4 * kp_dirs, f"4*{kp_dirs}*cells: {kp_dirs} directions "
+                        f"({'E, W; the others in k_sweep' if sweep else 'all but top-to-bottom'}), "
+                        f"C read + record write each"),
+            "k_sweep": (cells * 4, "4*cells: one C read + one record write per pass (halo re-reads excluded)"),
+            "k_south_wta": (cells * 2 * (1 + nrec), f"2*(1+{nrec})*cells: C + {nrec} records read"),
+        }
+        name = max((n for n in models if per_kind[n][1]), key=lambda n: per_kind[n][0])
+        tot_ms, cnt = per_kind[name]
+        bytes_per_launch, model = models[name]
         avg_s = tot_ms / cnt / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
+        label = {
+            "k_paths": f"k_paths<DPL={2 if D <= 128 else 4}> ({kp_dirs} of the {P} path directions of a batch in "
+                       f"one launch; the top-to-bottom one is fused into k_south_wta)",
+            "k_sweep": "k_sweep (row-synchronous up/down passes of batched MODE_HH)",
+            "k_south_wta": f"k_south_wta (top-to-bottom path fused with the WTA, reading {nrec} records)",
+        }[name]
         roof = {
             "bound": "hbm",
-            "kernel": f"k_paths<DPL={2 if D <= 128 else 4}> ({P - 1} of the {P} path directions of a batch "
-                      f"in one launch; the top-to-bottom one is fused into k_south_wta)",
+            "kernel": label,
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(f"{a.config}:k_paths"),
+            "traffic": load_traffic(f"{a.config}:{name}"),
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "bytes_model": f"4*(P-1)*cells, P={P}, cells=batch*H*W1*D={cells}",
+            "bytes_model": f"{model}; cells=batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),
             "launches_timed": cnt,
             "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
         }
-        # whole pipeline against the canonical 2+6P B/cell model (cost write, path C read +
-        # L write, WTA L read), over the summed kernel time of one step
-        pipe_bytes = cells * (2 + 6 * P)
+        # whole pipeline: cost write + the path kernels' data flow above, over the summed kernel
+        # time of one step
+        pipe_bytes = cells * (2 + 4 * kp_dirs + (8 if sweep else 0) + 2 * (1 + nrec))
         gpu_s = all_ms / 1e3 / max(1, frames_seen)
         roof["pipeline"] = {
             "algorithmic_bytes_per_step": pipe_bytes,

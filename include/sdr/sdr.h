@@ -375,7 +375,8 @@ enum {
     SDR_KERNEL_PREFILTER = 0, SDR_KERNEL_COST = 1, SDR_KERNEL_PATHS = 2,
     SDR_KERNEL_WTA_LR = 3,   /* k_south_wta: top-to-bottom path fused with WTA/uniqueness/disp2 */
     SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6,
-    SDR_KERNEL_LR_CHECK = 7  /* k_lr_check */
+    SDR_KERNEL_LR_CHECK = 7, /* the LR-checked map materialised (debug stage 2 only since round 3) */
+    SDR_KERNEL_SWEEP = 8     /* k_sweep: batched MODE_HH's up (N, NE, NW) and down (SE, SW) passes */
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);

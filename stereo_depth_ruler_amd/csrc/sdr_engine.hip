@@ -636,7 +636,6 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     { KTimer kt(h, SDR_KERNEL_PATHS); sdr::launch_paths(g, pls, F, st); }
     if (sweep) {
-        KTimer kt(h, SDR_KERNEL_PATHS);
         char* sb = (char*)h->sweep.p;
         SDR_HIP(hipMemsetAsync(sb, 0, sweep_flags + sizeof(int), st));
         sdr::SweepArgs sa{};
@@ -656,6 +655,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             sa.ntiles = shp[up].ntiles;
             sa.nslots = shp[up].nslots;
             sa.rec = Lr + (size_t)(up ? 2 : 3) * g.D;
+            KTimer kt(h, SDR_KERNEL_SWEEP);
             sdr::launch_sweep(g, sa, F, st);
             sa.flags += flags_n[up];
         }

@@ -32,7 +32,7 @@ MODE_SGBM, MODE_HH, MODE_SGBM_3WAY, MODE_HH4 = 0, 1, 2, 3
 UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
 # SDR_KERNEL_* (include/sdr/sdr.h)
 (KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATHS, KERNEL_WTA_LR, KERNEL_MEDIAN, KERNEL_SPECKLE,
- KERNEL_REPROJECT, KERNEL_LR_CHECK) = range(8)
+ KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP) = range(9)
 
 
 def _is_cuda(x) -> bool:

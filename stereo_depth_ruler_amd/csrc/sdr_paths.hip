@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
                     Regs<K> p = j > 0 ? La[j > 0 ? j - 1 : 0] : inA;
                     uint32_t dp = j > 0 ? da[j > 0 ? j - 1 : 0] : dinA;
                     uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    const Regs<K> L = path_step<K, PAD, false>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                    const Regs<K> L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
                     La[j] = L;
                     da[j] = dp;
                     const bool o = j == ncol - 1;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
                     for (int i = 0; i < K; i++) p.r[i] = in ? Lb[j + 1 < NC ? j + 1 : NC - 1].r[i] : inB.r[i];
                     uint32_t dp = in ? db[j + 1 < NC ? j + 1 : NC - 1] : dinB;
                     uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    const Regs<K> L = path_step<K, PAD, false>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                    const Regs<K> L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
                     Lb[j] = L;
                     db[j] = dp;
                     if (sum) {
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
 #pragma unroll
                     for (int j = 0; j < NC; j++) {
                         uint32_t upr = kMaxPair, dnr = kMaxPair;
-                        sum[j] = path_step<K, PAD, false>(c[j], Lv[j], dv[j], P1x2, P2x2, active, upr, dnr);
+                        sum[j] = path_step<K, PAD, true>(c[j], Lv[j], dv[j], P1x2, P2x2, active, upr, dnr);
                     }
                 }
                 diag_a(inA, dinA, sum);

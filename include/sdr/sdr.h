@@ -393,7 +393,8 @@ int sdr_selftest_wave_ops(int* failures4);
  * [P-1][F][H][W1][D] s16 (every direction but top-to-bottom, whose L is consumed on chip by the
  * fused WTA pass), 5 = the right view's WTA keys [F][H][W] u32: (minS << 16 | 0xffff - x) of the
  * winning left pixel x (matched column) per right-view column, 0xffffffff where none (not built
- * when the LR check cannot fire); stage 1 holds values only in the matched columns. */
+ * when the LR check cannot fire), 6 = MODE_SGBM_3WAY's stripe-start cost rows [F][stripes][rows][W1][D]
+ * s16 (rows = the largest stripe's count); stage 1 holds values only in the matched columns. */
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* host_dst, size_t bytes);
 
 /* Page-locked host memory (the role of cv::cuda::HostMem): host buffers from sdr_host_alloc that

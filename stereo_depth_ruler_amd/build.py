@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libsdr.so")
-SOURCES = ["sdr_cost.hip", "sdr_cost3.hip", "sdr_cost3k2.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_rectify.hip",
+SOURCES = ["sdr_cost.hip", "sdr_cost3.hip", "sdr_cost3k2.hip", "sdr_cost_generic.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_rectify.hip",
            "sdr_cloud.hip", "sdr_display.hip", "sdr_engine.hip"]
 HEADERS = ["sdr_device.hpp", "sdr_internal.hpp", "sdr_cost_kernel.hpp"]
 ARCH = os.environ.get("SDR_OFFLOAD_ARCH", "gfx950")

@@ -83,7 +83,6 @@ int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     e->speckle_ws = p.speckleWindowSize;
     e->speckle_diff = 16 * p.speckleRange;
     e->blockSize = p.blockSize;
-    if (g.SH2 > 5 || g.SW2 > 5) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
     // The int16 domain of OpenCV's own arithmetic: C = P2 + block cost and delta = minLp + P2
     // (minLp <= C) must fit a short.  Past it OpenCV's SIMD build wraps (short)delta0 and
     // saturates C while its scalar build computes them in int, so the reference's output is not
@@ -114,7 +113,7 @@ int check_frame(const Eff& e) {
     // k_cost addresses a frame's right-image planes (3 x 8 B per pixel) the same way
     if ((size_t)g.H * g.W * 24 > (size_t)INT32_MAX)
         return fail(SDR_ERR_SIZE, "frame too large: the right image's cost planes span more than 2 GiB");
-    if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "blockSize > 11 is not supported");
+    if (!sdr::cost_supported(g)) return fail(SDR_ERR_LIMIT, "numDisparities > 256 is not supported");
     return SDR_OK;
 }
 
@@ -346,6 +345,7 @@ struct sdr_sgbm {
     bool lr_skipped = false;
     sdr::Geometry lr_g{};
     int lr_frames = 0, lr_d12 = 0;
+    size_t aux_slack = 0;  // elements before the 3WAY stripe-start rows in Caux
 };
 
 namespace {
@@ -497,7 +497,9 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     if ((rc = ensure(h->C, (F * cells + 2 * slack) * 2))) return rc;
     if ((rc = ensure(h->Lr, (F * lfs + 2 * lslack) * 2))) return rc;
     if ((rc = ensure(h->keys2, F * px * 4))) return rc;
-    if ((rc = ensure(h->Caux, F * aux_fstride * 2))) return rc;
+    // the E/W chains redirected into it (RowRedirect) load up to a lookahead past a row's ends
+    const size_t aux_slack = (size_t)sdr::kSouthPad * g.D;
+    if ((rc = ensure(h->Caux, (F * aux_fstride + 2 * aux_slack) * 2))) return rc;
     if ((rc = ensure(h->draw, F * px * 2))) return rc;
     if ((rc = ensure(h->dlr, F * px * 2))) return rc;
     if (e.speckle_ws > 0) {
@@ -509,7 +511,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     h->path_slack = slack;
     h->path_lslack = lslack;
     int16_t* C = (int16_t*)h->C.p + slack;
-    int16_t* Caux = (int16_t*)h->Caux.p;
+    int16_t* Caux = (int16_t*)h->Caux.p + aux_slack;
+    h->aux_slack = aux_slack;
     int16_t* Lr = (int16_t*)h->Lr.p + lslack;  // [F][H][W1][nrec][D]
     // [pass][slots][tiles][2] counters, the error word, then the edge ring (sized for either pass)
     size_t flags_n[2] = {0, 0}, edge_bytes = 0;
@@ -572,7 +575,12 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         x.s0 = sp.s0;
         x.ylim = sp.ylim;
     }
-    { KTimer kt(h, SDR_KERNEL_COST); sdr::launch_cost(g, ca, F, st); }
+    {
+        KTimer kt(h, SDR_KERNEL_COST);
+        // blockSize 13..17 (within the int16 domain): the two-pass cost through the idle L records
+        if (g.SH2 > 5) sdr::launch_cost_generic(g, ca, F, (uint32_t*)h->Lr.p, st);
+        else sdr::launch_cost(g, ca, F, st);
+    }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));
 
     // k_paths: every direction except the top-to-bottom one, each into its own L buffer (in the
@@ -629,6 +637,17 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             add_dir(pls, sdr::DIR_NE, nD, buf());
             add_dir(pls, sdr::DIR_NW, nD, buf());
         }
+    }
+    for (size_t s = 0; s < stripes.size(); s++) {
+        const Stripe& sp = stripes[s];
+        // every row of the stripe comes from its own buffer: its output rows differ from C too
+        if (sp.aux_rows == 0 || sp.aux_rows != sp.end - sp.s0 || sp.out0 >= sp.end) continue;
+        if (pls.nredir == sdr::kMaxCostAux) return fail(SDR_ERR_ARG, "too many 3WAY stripes");
+        sdr::RowRedirect& r = pls.redir[pls.nredir++];
+        r.lo = sp.out0;
+        r.hi = sp.end;
+        r.s0 = sp.s0;
+        r.aux = Caux + s * (size_t)amax * g.W1 * g.D;
     }
     for (sdr::PathLaunch* pl : {&pls, &plS}) {
         pl->prefix[0] = 0;
@@ -1300,10 +1319,12 @@ int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int*
 int sdr_sgbm_debug_stage(const sdr_sgbm* h, int stage, void* dst, size_t bytes) {
     if (!h || !dst) return fail(SDR_ERR_ARG, "null argument");
     const Buf* b = stage == 0 ? &h->C : stage == 1 ? &h->draw : stage == 2 ? &h->dlr
-                 : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : stage == 5 ? &h->keys2 : nullptr;
+                 : stage == 3 ? &h->dfin : stage == 4 ? &h->Lr : stage == 5 ? &h->keys2
+                 : stage == 6 ? &h->Caux : nullptr;
     if (!b) return fail(SDR_ERR_ARG, "bad stage");
     // front slack (the L records' is P-1 times C's)
-    const size_t skip = stage == 0 ? h->path_slack * 2 : stage == 4 ? h->path_lslack * 2 : 0;
+    const size_t skip = stage == 0 ? h->path_slack * 2 : stage == 4 ? h->path_lslack * 2
+                      : stage == 6 ? h->aux_slack * 2 : 0;
     if (!b->p || bytes + skip > b->n) return fail(SDR_ERR_ARG, "stage buffer smaller than requested");
     SDR_HIP(hipSetDevice(h->device));
     // the LR-checked map is never written by the pipeline: materialise it for this stage

@@ -113,6 +113,15 @@ struct PathDir {
 // The path costs of the P-1 directions k_paths writes are stored pixel-interleaved,
 // L[F][H][W1][P-1][D]: the fused WTA pass then reads one contiguous (P-1)*D record per pixel
 // instead of P-1 streams a whole volume apart.
+// MODE_SGBM_3WAY: a stripe whose rows all keep their window clamped at the stripe start (the short
+// last stripes, where H-1-SH2 < s0 + SH2: every row's window is frozen above s0 + SH2) has cost
+// rows that differ from C on its output rows too; OpenCV runs that stripe's horizontal passes on
+// its own rows, so the E/W chains of rows [lo, hi) read stripe row y - s0 of aux instead of C
+struct RowRedirect {
+    int lo, hi, s0;
+    const int16_t* aux;  // [F][rows][W1][D], frames PathLaunch::aux_fstride apart
+};
+
 struct PathLaunch {
     const int16_t* C;
     size_t cs_fstride;   // elements per frame of C
@@ -122,6 +131,8 @@ struct PathLaunch {
     int ndirs;
     int prefix[kMaxPathDirs + 1];  // chain prefix sums
     PathDir d[kMaxPathDirs];
+    int nredir;
+    RowRedirect redir[kMaxCostAux];
 };
 
 // Row-synchronous sweeps of batched MODE_HH (sdr_paths.hip, k_sweep): the upward directions N, NE
@@ -219,6 +230,10 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
                       uint32_t* d2fill = nullptr);
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
+// blockSize > 11 (SH2 > 5, sdr_cost_generic.hip): two passes through a scratch volume h1 of
+// cost_generic_scratch_bytes (the L-record buffer, idle until the path kernels)
+size_t cost_generic_scratch_bytes(const Geometry& g, int F);
+void launch_cost_generic(const Geometry& g, const CostArgs& a, int F, uint32_t* h1, hipStream_t st);
 void launch_cost_cn3(const Geometry& g, const CostArgs& a, int F, hipStream_t st);  // pl.cn == 3
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st);
 void launch_median3(const int16_t* src, int16_t* dst, int W, int H, int F, hipStream_t st);

@@ -141,6 +141,13 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     const ptrdiff_t rowb = (ptrdiff_t)(ch.dy * W1 + ch.dx) * D * 2;          // C, per step
     const ptrdiff_t rowl = (ptrdiff_t)(ch.dy * W1 + ch.dx) * pl.l_pix * 2;   // L records, per step
     const char* cp = (const char*)(pl.C + (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D);
+    if (pd.dir == DIR_E || pd.dir == DIR_W) {
+        // a short last 3WAY stripe's output rows: its own cost rows (RowRedirect)
+        for (int i = 0; i < pl.nredir; i++)
+            if (ch.y0 >= pl.redir[i].lo && ch.y0 < pl.redir[i].hi)
+                cp = (const char*)(pl.redir[i].aux + (size_t)f * pl.aux_fstride +
+                                   ((size_t)(ch.y0 - pl.redir[i].s0) * W1 + ch.x0) * D);
+    }
     char* op = (char*)(pd.out + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
     const int last = ch.len - 1;
     // C: one resource for the whole chain, based at the lowest address the chain's loads touch

@@ -94,6 +94,50 @@ def test_edge_cases_bit_exact(oracle, kind, H, W, args):
         check_case(oracle, kind, H, W, args, uniq_rule=rule, seed=H * W)
 
 
+@st.composite
+def wide_block_cases(draw):
+    """blockSize 13..17: the engine's two-pass cost path (k_hsum_generic / k_vsum_generic)."""
+    mode = draw(st.sampled_from([0, 1, 2]))
+    bs = draw(st.sampled_from([13, 15, 17]))
+    D = 16 * draw(st.integers(1, 16))
+    minD = draw(st.integers(-30, 8))
+    H = draw(st.integers(4, 40))
+    W1 = draw(st.integers(bs // 2 + 1, 120))
+    W = W1 - min(minD, 0) + max(minD + D, 0)
+    cap = draw(st.sampled_from([c for c in (15, 21, 31) if p2_domain_max(bs, c, mode) >= 64]))
+    pmax = p2_domain_max(bs, cap, mode)
+    P1 = draw(st.integers(1, max(1, min(pmax - 1, 2000))))
+    P2 = draw(st.one_of(st.just(pmax), st.integers(P1 + 1, max(P1 + 1, pmax))))
+    kind = draw(st.sampled_from(S.ADVERSARIAL_KINDS))
+    return dict(kind=kind, H=H, W=W, args=(minD, D, bs, P1, P2, draw(st.sampled_from([1, 1000000])), cap,
+                                            draw(st.sampled_from([0, 10])), draw(st.sampled_from([0, 30])), 2, mode),
+                nstripes=draw(st.sampled_from([1, 3, 4])), uniq_rule=draw(st.integers(0, 2)),
+                seed=draw(st.integers(0, 10**6)))
+
+
+@settings(max_examples=30, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(case=wide_block_cases())
+def test_wide_blocks_bit_exact(oracle, case):
+    check_case(oracle, case["kind"], case["H"], case["W"], case["args"], case["nstripes"],
+               case["uniq_rule"], case["seed"])
+
+
+@pytest.mark.parametrize("bs,mode", [(13, 0), (15, 1), (17, 2), (17, 1), (13, 2)])
+def test_wide_blocks_domain_edge(oracle, bs, mode):
+    """The largest P2 of the int16 domain at 1280-class widths (binary pairs: saturated sums)."""
+    args = (0, 128, bs, 81, p2_domain_max(bs, 15, mode), 1, 15, 10, 50, 2, mode)
+    check_case(oracle, "binary", 36, 300, args, seed=bs)
+    check_case(oracle, "textured", 60, 360, args, seed=bs + 1)
+
+
+def test_block_19_is_outside_the_domain():
+    L = np.zeros((30, 120), np.uint8)
+    with pytest.raises(sdr.SDRError) as e:
+        sdr.StereoSGBM.create(0, 16, 19, 1, 2, 1, 15).compute(L, L)
+    assert e.value.code == -8
+
+
 def test_outside_int16_domain_is_refused():
     L = np.zeros((20, 100), np.uint8)
     pmax = p2_domain_max(5, 63, 0)
@@ -120,3 +164,15 @@ def test_one_matcher_two_streams(oracle):
     p = oracle.make_params(*args)
     for (a, b), o in zip(pairs, outs):
         assert np.array_equal(o.cpu().numpy(), oracle.sgbm_compute(a, b, p))
+
+
+@pytest.mark.parametrize("bs", [7, 9, 11, 13, 17])
+def test_3way_short_last_stripes(oracle, bs):
+    """MODE_SGBM_3WAY stripes whose every row keeps its window clamped at the stripe start (H-1-SH2
+    < s0 + SH2, the short last stripes of small frames at larger block sizes): their output rows'
+    horizontal passes run on the stripe's own cost rows (a round-3 fix; found by the wide-block
+    tests)."""
+    for H in (14, 15, 17, 18, 21, 26):
+        for ns in (4, 8):
+            args = (0, 32, bs, 10, 500, 1, 15, 10, 0, 2, 2)
+            check_case(oracle, "noise", H, 90, args, nstripes=ns, seed=H)

@@ -153,3 +153,24 @@ def test_hh4_differs_from_hh(oracle):
     hh4 = oracle.sgbm_compute(L, R, oracle.make_params(*args))
     args[10] = 1
     assert (hh4 != oracle.sgbm_compute(L, R, oracle.make_params(*args))).sum() > 0
+
+
+# blockSize 13..17 (past k_cost's register ring: the engine's two-pass cost path): only small
+# preFilterCap keeps them inside the int16 domain ((2*15 + 63) * 17^2 = 26877); 19 never fits
+WIDE_CASES = [(bs, mode, kind, seed) for seed, (bs, mode, kind) in enumerate(
+    [(13, 0, "textured"), (15, 1, "noise"), (17, 2, "binary"), (13, 2, "steps"), (17, 0, "periodic"),
+     (15, 2, "flat")])]
+
+
+@pytest.mark.parametrize("bs,mode,kind,seed", WIDE_CASES)
+def test_oracle_wide_blocks_match_volume_formulation(oracle, bs, mode, kind, seed):
+    D, minD = 32, (0 if seed % 2 else -6)
+    H, W = 30 + seed, D + max(minD, 0) + 60
+    P2 = p2_domain_max(bs, 15, mode)
+    assert P2 > 20
+    args = (minD, D, bs, 10, min(P2, 1200), 1, 15, 10, (30 if seed % 2 else 0), 2, mode)
+    L, R = S.adversarial_pair(kind, H, W, D, seed=seed)
+    for stages in (0, 3):
+        ref = oracle.sgbm_compute(L, R, oracle.make_params(*args), stages=stages)
+        got = N.sgm_full_volume(L, R, *args, stages=stages)
+        assert np.array_equal(ref, got), f"stages={stages}: {(ref != got).sum()} px differ"

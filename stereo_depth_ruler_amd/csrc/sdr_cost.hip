@@ -152,8 +152,8 @@ namespace sdr {
 // one output row of the widest column-block span (racing garbage from every block)
 size_t cost_sink_bytes(const Geometry& g) { return (size_t)(g.W1 + 64) * g.D * 2; }
 
-// SH2 <= 5: k_cost (one pass, register ring); larger windows: launch_cost_generic
-bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.D <= 256; }
+// SH2 <= 5 and D <= 256: k_cost (one pass, register ring); otherwise launch_cost_generic
+bool cost_supported(const Geometry& g) { return g.SH2 == g.SW2 && g.D <= 512; }
 
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st) {
     if (a.row_end <= a.row_begin && a.naux == 0) return;

@@ -47,7 +47,7 @@ struct Eff {
 int make_eff(const sdr_sgbm_params& p, int W, int H, Eff* e) {
     if (p.numDisparities <= 0 || p.numDisparities % 16 != 0)
         return fail(SDR_ERR_NUMDISP, "numDisparities must be positive and divisible by 16");
-    if (p.numDisparities > 256) return fail(SDR_ERR_LIMIT, "numDisparities > 256 is not supported");
+    if (p.numDisparities > 512) return fail(SDR_ERR_LIMIT, "numDisparities > 512 is not supported");
     if (p.mode != SDR_MODE_SGBM && p.mode != SDR_MODE_HH && p.mode != SDR_MODE_SGBM_3WAY &&
         p.mode != SDR_MODE_HH4)
         return fail(SDR_ERR_MODE, "unknown mode");
@@ -113,7 +113,7 @@ int check_frame(const Eff& e) {
     // k_cost addresses a frame's right-image planes (3 x 8 B per pixel) the same way
     if ((size_t)g.H * g.W * 24 > (size_t)INT32_MAX)
         return fail(SDR_ERR_SIZE, "frame too large: the right image's cost planes span more than 2 GiB");
-    if (!sdr::cost_supported(g)) return fail(SDR_ERR_LIMIT, "numDisparities > 256 is not supported");
+    if (!sdr::cost_supported(g)) return fail(SDR_ERR_ARG, "unsupported block shape");
     return SDR_OK;
 }
 
@@ -577,8 +577,9 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     {
         KTimer kt(h, SDR_KERNEL_COST);
-        // blockSize 13..17 (within the int16 domain): the two-pass cost through the idle L records
-        if (g.SH2 > 5) sdr::launch_cost_generic(g, ca, F, (uint32_t*)h->Lr.p, st);
+        // blockSize 13..17 (within the int16 domain) or D > 256: the two-pass cost through the
+        // idle L records
+        if (g.SH2 > 5 || g.D > 256) sdr::launch_cost_generic(g, ca, F, (uint32_t*)h->Lr.p, st);
         else sdr::launch_cost(g, ca, F, st);
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[1], st));

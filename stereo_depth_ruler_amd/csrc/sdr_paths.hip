@@ -101,8 +101,9 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
 // k_paths lookahead (steps).  32 steps at D <= 128 measured slower on the class path's 640x360
 // frames (k_paths 75 -> 82 us for both matchers; C2 unchanged): its E/W chains wait on the
 // memory system (3.4 TB/s over the launch), not on the lookahead.
+// (8 at D > 256: four pairs per lane, a 16-slot ring is already 64 VGPRs)
 template <int DPL>
-constexpr int paths_la() { return 16; }
+constexpr int paths_la() { return DPL == 8 ? 8 : 16; }
 // k_paths loads C with the default cache policy: the launch's four directions (and k_south_wta
 // after it) re-read C, and the 212 MB volume of a C2 frame is served partly from the 256 MB
 // Infinity Cache -- non-temporal C loads there measured 274 -> 340 us.
@@ -206,9 +207,12 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
     if (g.D <= 128) {
         if (g.D < 128) hipLaunchKernelGGL((k_paths<2, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<2, false>), grid, dim3(256), 0, st, g, pl);
-    } else {
+    } else if (g.D <= 256) {
         if (g.D < 256) hipLaunchKernelGGL((k_paths<4, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<4, false>), grid, dim3(256), 0, st, g, pl);
+    } else {
+        if (g.D < 512) hipLaunchKernelGGL((k_paths<8, true>), grid, dim3(256), 0, st, g, pl);
+        else hipLaunchKernelGGL((k_paths<8, false>), grid, dim3(256), 0, st, g, pl);
     }
 }
 
@@ -496,7 +500,7 @@ static int sweep_occupancy() {
 
 SweepShape sweep_shape(const Geometry& g, int F, bool up) {
     SweepShape sh{0, 0, 0};
-    if (g.W1 <= 0 || F <= 0) return sh;
+    if (g.W1 <= 0 || F <= 0 || g.D > 256) return sh;  // four pairs per lane do not fit its registers
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -653,8 +657,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     // ---------------- consumers: the other directions + WTA, RPW rows per wave ----------------
     constexpr int NPASS = kSouthRPW / 4;  // passes of 4 rows (one per 16-lane group)
     const int gl = lane & 15, grp = lane >> 4;
+    // D > 256: 32 disparities per lane, so the last active lane may hold fewer than 32 (D is a
+    // multiple of 16): it reads its own offset and masks the pairs past D (see ssum)
     const bool wactive = !PAD || gl * WDPL < D;
-    const int wd0 = (PAD ? min(gl, D / WDPL - 1) : gl) * WDPL;
+    const int wd0 = (PAD ? min(gl, (D - 1) / WDPL) : gl) * WDPL;
     // row blk*RB + r of the chain: wave-uniform block base + lane byte offset; the NP
     // directions of a pixel are one contiguous record (q*D*2 folds into the instruction offset)
     const ptrdiff_t bstepb = (ptrdiff_t)RB * W1 * pl.l_pix * 2;
@@ -713,6 +719,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
                 const uint32_t v = p == kSouthIdx ? ls[i] : o[p < kSouthIdx ? p : p - 1].r[i];
                 acc = p == 0 ? v : pk_add_sat(acc, v);
             }
+            if constexpr (PAD && DPL == 8) acc = wd0 + 2 * i < D ? acc : kMaxPair;  // past D: never a minimum
             St.r[i] = acc;
         }
         return St;
@@ -840,9 +847,12 @@ void launch_south_wta(const Geometry& g, const PathLaunch& pl, const SouthWtaArg
     if (g.D <= 128) {
         if (g.D < 128) launch_south_np<2, true>(g, pl, a, F, st);
         else launch_south_np<2, false>(g, pl, a, F, st);
-    } else {
+    } else if (g.D <= 256) {
         if (g.D < 256) launch_south_np<4, true>(g, pl, a, F, st);
         else launch_south_np<4, false>(g, pl, a, F, st);
+    } else {
+        if (g.D < 512) launch_south_np<8, true>(g, pl, a, F, st);
+        else launch_south_np<8, false>(g, pl, a, F, st);
     }
 }
 

@@ -41,7 +41,7 @@ def check_case(oracle, kind, H, W, args, nstripes=4, uniq_rule=0, seed=0):
 @st.composite
 def sgbm_cases(draw):
     mode = draw(st.sampled_from([0, 1, 2]))
-    D = 16 * draw(st.integers(1, 16))
+    D = 16 * draw(st.integers(1, 32))  # up to 512 (four pairs per lane past 256)
     bs = draw(st.sampled_from([1, 3, 5, 7, 9, 11]))
     minD = draw(st.integers(-40, 8))
     H = draw(st.integers(4, 48))
@@ -176,3 +176,43 @@ def test_3way_short_last_stripes(oracle, bs):
         for ns in (4, 8):
             args = (0, 32, bs, 10, 500, 1, 15, 10, 0, 2, 2)
             check_case(oracle, "noise", H, 90, args, nstripes=ns, seed=H)
+
+
+# numDisparities 272..512 (round 3): four disparity pairs per lane in k_paths / the fused WTA
+# (its consumers' last lane masked past D), the two-pass cost path, no row sweeps
+WIDE_D = [
+    # kind, H, W, (minD, D, bs, P1, P2, d12, cap, uniq, ws, sr, mode), nstripes
+    ("textured", 40, 620, (0, 512, 5, 600, 2400, 1, 63, 10, 100, 2, 0), 4),
+    ("noise", 30, 400, (-20, 272, 3, 8, 200, 1, 31, 5, 0, 0, 1), 4),
+    ("binary", 24, 420, (0, 304, 5, 81, p2_domain_max(5, 63, 2), 1000000, 63, 15, 0, 0, 2), 3),
+    ("periodic", 20, 520, (0, 384, 7, 50, 1500, 2, 31, 10, 30, 1, 0), 4),
+    ("steps", 36, 600, (-5, 496, 1, 10, 100, 1, 63, 0, 0, 0, 3), 4),
+    ("textured", 50, 700, (0, 448, 9, 300, 2400, 1, 15, 12, 50, 2, 1), 4),
+]
+
+
+@pytest.mark.parametrize("kind,H,W,args,ns", WIDE_D, ids=[f"{w[0]}_D{w[3][1]}_m{w[3][10]}" for w in WIDE_D])
+def test_wide_disparity_range_bit_exact(oracle, kind, H, W, args, ns):
+    for rule in (0, 2):
+        check_case(oracle, kind, H, W, args, nstripes=ns, uniq_rule=rule, seed=H + W)
+
+
+def test_wide_disparity_batch_and_colour(oracle):
+    """D = 320 on a batch of 3 CV_8UC3 frames: the colour operand sets through the two-pass cost."""
+    dev = torch.device("cuda", 0)
+    args = (0, 320, 5, 600, 2400, 1, 31, 10, 0, 2, 0)
+    frames = [S.make_pair(30, 400, 320, seed=90 + i)[:2] for i in range(3)]
+    Lc = np.stack([np.stack([f[0], np.roll(f[0], 1, 1), 255 - f[0]], -1) for f in frames])
+    Rc = np.stack([np.stack([f[1], np.roll(f[1], 1, 1), 255 - f[1]], -1) for f in frames])
+    m = sdr.StereoSGBM.create(*args)
+    got = m.compute(torch.from_numpy(Lc).to(dev), torch.from_numpy(Rc).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    for i in range(3):
+        assert np.array_equal(got[i], oracle.sgbm_compute(Lc[i], Rc[i], p)), i
+
+
+def test_disparity_range_past_512_is_refused():
+    L = np.zeros((10, 700), np.uint8)
+    with pytest.raises(sdr.SDRError) as e:
+        sdr.StereoSGBM.create(0, 528, 5, 10, 100, 1, 63).compute(L, L)
+    assert e.value.code == -8

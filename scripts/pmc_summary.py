@@ -69,16 +69,24 @@ def main():
     except FileNotFoundError:
         traffic = {}
     lines += ["", "HBM bytes per launch = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024:", ""]
+    # this tag's entries are replaced as a whole (kernels the pipeline no longer runs drop out);
+    # several instances of one kernel (k_sweep's up and down passes) average per launch
+    traffic = {key: v for key, v in traffic.items() if not key.startswith(a.tag + ":")}
+    per_base = collections.defaultdict(list)
     for k in kernels:
         f, w = avg.get((k, "FETCH_SIZE")), avg.get((k, "WRITE_SIZE"))
         if f is None or w is None:
             continue
         b = int(2 * f * 1024 + w * 1024)
-        base = k.split("<")[0]
-        traffic[f"{a.tag}:{base}"] = {"hbm_bytes_per_launch": b, "read_bytes": int(2 * f * 1024),
-                                      "write_bytes": int(w * 1024), "instance": k,
-                                      "source": os.path.basename(a.out) + ".md"}
+        per_base[k.split("<")[0]].append((k, b, int(2 * f * 1024), int(w * 1024)))
         lines.append(f"- {k}: {b / 1e9:.4f} GB (read {2 * f * 1024 / 1e9:.4f}, write {w * 1024 / 1e9:.4f})")
+    for base, inst in per_base.items():
+        n = len(inst)
+        traffic[f"{a.tag}:{base}"] = {"hbm_bytes_per_launch": sum(i[1] for i in inst) // n,
+                                      "read_bytes": sum(i[2] for i in inst) // n,
+                                      "write_bytes": sum(i[3] for i in inst) // n,
+                                      "instance": " + ".join(i[0] for i in inst),
+                                      "source": os.path.basename(a.out) + ".md"}
     with open(a.out + ".md", "w") as fh:
         fh.write("\n".join(lines) + "\n")
     with open(traffic_path, "w") as fh:

@@ -35,6 +35,7 @@ def _batch(kind, F, H, W, D, seed):
     ("binary", 8, 30, 120, 16, 0, 4),       # saturated S sums
     ("textured", 8, 26, 260, 160, 20, 5),   # DPL 4 with padded lanes
     ("steps", 10, 20, 100, 32, 0, 6),
+    ("textured", 8, 18, 192, 32, 0, 7),     # W1 = 160: whole tiles only (80 columns)
 ])
 def test_hh_sweep_batch_bit_exact(oracle, kind, F, H, W, D, speckle, seed):
     args = (0, D, 5, 600, 2400, 1, 63, 10, speckle, 2, sdr.MODE_HH)
@@ -52,4 +53,23 @@ def test_hh_sweep_batch_bit_exact(oracle, kind, F, H, W, D, speckle, seed):
         assert np.array_equal(m.compute(Ls[i], Rs[i]), out[i])
     again = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
     assert np.array_equal(again, out)
+    m.close()
+
+
+def test_hh_sweep_frames_per_slot_and_negative_min_disparity(oracle):
+    """Wide frames (W1 = 1652: 21 tiles of 80 columns, so about 12 frames fit the resident grid)
+    in a batch of 16: the slots take a second frame each (the edge counters run on across frames,
+    the frame-start waits), with minDisparity < 0 and the uniqueness / LR variations."""
+    F, H, W, D = 16, 12, 1700, 48
+    args = (-8, D, 5, 200, 1600, 2, 63, 5, 0, 2, sdr.MODE_HH)
+    Ls, Rs = _batch("noise", F // 2, H, W, D, 11)
+    L2, R2 = _batch("textured", F // 2, H, W, D, 30)
+    Ls, Rs = np.concatenate([Ls, L2]), np.concatenate([Rs, R2])
+    dev = torch.device("cuda", 0)
+    m = sdr.StereoSGBM.create(*args)
+    out = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    for i in range(F):
+        ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
+        assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
     m.close()

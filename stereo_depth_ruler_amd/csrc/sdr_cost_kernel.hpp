@@ -29,10 +29,15 @@ template <int NR, int K, int CN>
 struct CostCfg {
     static constexpr int SW2 = (NR - 1) / 2;
     static constexpr int BCOLS = K == 1 ? 32 : 16;  // output columns of a block
-    static constexpr int CW = BCOLS / 4;            // output columns per wave (horizontal sums)
+    // waves per block.  8 (a ring of 5 pixel-cost columns per wave instead of 9: 158 -> 120 VGPRs,
+    // 4 waves per SIMD instead of 3) measured slower on C2, 79.3 -> 85.3 us: the row barrier then
+    // syncs twice the waves and the horizontal sums read 2 halo columns per 4 outputs, not per 8
+    static constexpr int NW = 4;
+    static constexpr int NT = 64 * NW;              // threads per block
+    static constexpr int CW = BCOLS / NW;           // output columns per wave (horizontal sums)
     static constexpr int NPB = BCOLS + 2 * SW2;     // pixel-cost columns the block needs
-    static constexpr int PCW = (NPB + 3) / 4;       // pixel-cost columns per wave: p = wave + 4*jj
-    static constexpr int NLV = 4 * PCW;             // staged virtual columns
+    static constexpr int PCW = (NPB + NW - 1) / NW;  // pixel-cost columns per wave: p = wave + NW*jj
+    static constexpr int NLV = NW * PCW;             // staged virtual columns
     // row prefetch depth and the row loop's unroll: U covers the ring slot (% NR), the LDS
     // double buffer (% 2) and the prefetch register slot (% PD) statically
     // (two rows: deeper prefetch costs registers, i.e. resident blocks, and measured slower)
@@ -133,7 +138,8 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
     // a guarded load makes hipcc branch around it and wait vmcnt(0) right after it is issued.
     // Staging goes through registers, not LDS-direct loads, because the barrier of every row
     // would then wait for all of them.
-    constexpr int NPR = K;  // R entries per thread per plane: NRP <= 256 * K
+    constexpr int NT = Cfg::NT, NW = Cfg::NW;
+    constexpr int NPR = (NLV + 128 * K - 2 + NT - 1) / NT;  // R entries per thread per plane (NRP <= NLV + D - 2)
     const int xr0 = g.minX1 + vlo - g.minD - (D - 2);
     const Rsrc rR = rsrc_at(a.pl.R + (size_t)f * a.pl.fstrideR);  // < 2 GiB a frame (check_frame)
     const Rsrc rL = rsrc_at(a.pl.L + (size_t)f * a.pl.fstrideL);
@@ -141,18 +147,18 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
     int pr[NPR];
 #pragma unroll
     for (int t = 0; t < NPR; t++) {
-        const int ir = min(tid + 256 * t, NRP - 1);
+        const int ir = min(tid + NT * t, NRP - 1);
         gr[t] = 8 * min(max(xr0 + ir, 0), W - 1);
         pr[t] = (ir & 1) * HR + (ir >> 1);
     }
     // L word il: column il / 3CN, word il % 3CN (operand set w / 3), staged as 4 words per
     // column and operand set (one 16-byte broadcast)
-    constexpr int NLT = (3 * CN * NLV + 255) / 256;  // L words per thread
+    constexpr int NLT = (3 * CN * NLV + NT - 1) / NT;  // L words per thread
     uint32_t gl[NLT];
     int pl[NLT];
 #pragma unroll
     for (int t = 0; t < NLT; t++) {
-        const int il = min(tid + 256 * t, 3 * CN * NLV - 1), c = il / (3 * CN), w = il % (3 * CN);
+        const int il = min(tid + NT * t, 3 * CN * NLV - 1), c = il / (3 * CN), w = il % (3 * CN);
         gl[t] = 4 * (3 * CN * (g.minX1 + min(max(vlo + c, 0), W1 - 1)) + w);
         pl[t] = (c * CN + w / 3) * 4 + w % 3;
     }
@@ -185,7 +191,7 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
     };
 
     // per-lane staged R position of this wave's column jj: (p & 1) * HR + p / 2 + (D-2)/2 - qp
-    // with p = wave + 4*jj, i.e. rpos + 2*jj (interleaved columns: one base register; a wave
+    // with p = wave + NW*jj, i.e. rpos + (NW/2)*jj (interleaved columns: one base register; a wave
     // owning contiguous columns needs two, and hipcc then spends ~40 more VGPRs on the row loop)
     int rpos[K];
 #pragma unroll
@@ -269,13 +275,13 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
 #pragma unroll
             for (int ch = 0; ch < CN; ch++) {
                 // operand set ch (colour: channel ch's Sobel and raw costs add up)
-                const u32x4 lw = BL[4 * jj * CN + ch];
+                const u32x4 lw = BL[NW * jj * CN + ch];
                 const uint32_t w0 = lw.x, w1 = lw.y, w2 = lw.z;
                 const uint32_t u = half_lo(w0), u0 = half_hi(w0), u1 = half_lo(w1);
                 const uint32_t ur = half_hi(w1), ur0 = half_lo(w2), ur1 = half_hi(w2);
 #pragma unroll
                 for (int i = 0; i < K; i++) {
-                    const uint64_t* BRj = BR + rpos[i] + 2 * jj + 6 * ch * HR;
+                    const uint64_t* BRj = BR + rpos[i] + (NW / 2) * jj + 6 * ch * HR;
                     const uint64_t r0 = BRj[0], r1 = BRj[2 * HR], r2 = BRj[4 * HR];
                     const uint32_t bs = bt_cost(u, u0, u1, (uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1);
                     const uint32_t br = bt_cost(ur, ur0, ur1, (uint32_t)(r1 >> 32), (uint32_t)r2, (uint32_t)(r2 >> 32));
@@ -295,7 +301,7 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
 #pragma unroll
             for (int jj = 0; jj < PCW; jj++)
 #pragma unroll
-                for (int i = 0; i < K; i++) Vb[(4 * jj * K + i) * 64] = vs[i][jj];
+                for (int i = 0; i < K; i++) Vb[(NW * jj * K + i) * 64] = vs[i][jj];
         }
         __syncthreads();
     };
@@ -309,7 +315,7 @@ __device__ __forceinline__ void cost_block(const Geometry& g, const CostArgs& a,
 }
 
 template <int NR, int K, int CN>
-__global__ __launch_bounds__(256) void k_cost(Geometry g, CostArgs a) {
+__global__ __launch_bounds__((CostCfg<NR, K, CN>::NT)) void k_cost(Geometry g, CostArgs a) {
     using Cfg = CostCfg<NR, K, CN>;
     extern __shared__ uint64_t lds[];
     // column blocks of one row band are consecutive logical blocks: they share an XCD, so the
@@ -357,7 +363,7 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
             int dev = 0, cus = 0, per_cu = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_cost<NR, K, CN>, 256, lds);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_cost<NR, K, CN>, Cfg::NT, lds);
             slots = max(1, cus * max(1, per_cu));
             key = lds;
         }
@@ -371,7 +377,7 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
     }
     if (rows == 0) a.TY = 1;
     dim3 grid(colblocks, (rows + a.TY - 1) / a.TY + a.naux, F);
-    hipLaunchKernelGGL((k_cost<NR, K, CN>), grid, dim3(256), lds, st, g, a);
+    hipLaunchKernelGGL((k_cost<NR, K, CN>), grid, dim3(Cfg::NT), lds, st, g, a);
 }
 
 }  // namespace sdr

@@ -52,7 +52,7 @@ enum {
     SDR_ERR_TYPE = -5,        /* channels other than 1 or 3 (CV_8UC1 / CV_8UC3) */
     SDR_ERR_DEVICE = -6,      /* HIP runtime error */
     SDR_ERR_NOMEM = -7,
-    SDR_ERR_LIMIT = -8        /* numDisparities > 256 (engine limit) */
+    SDR_ERR_LIMIT = -8        /* numDisparities > 512, or outside the int16 cost domain */
 };
 
 /* Field order and meaning of cv::StereoSGBM::create(...) + two knobs OpenCV fixes internally. */

@@ -230,7 +230,7 @@ void launch_prefilter(const uint8_t* L, const uint8_t* R, size_t stride, size_t 
                       uint32_t* d2fill = nullptr);
 bool cost_supported(const Geometry& g);
 void launch_cost(const Geometry& g, const CostArgs& a, int F, hipStream_t st);
-// blockSize > 11 (SH2 > 5, sdr_cost_generic.hip): two passes through a scratch volume h1 of
+// blockSize > 11 (SH2 > 5) or D > 256 (sdr_cost_generic.hip): two passes through a scratch volume h1 of
 // cost_generic_scratch_bytes (the L-record buffer, idle until the path kernels)
 size_t cost_generic_scratch_bytes(const Geometry& g, int F);
 void launch_cost_generic(const Geometry& g, const CostArgs& a, int F, uint32_t* h1, hipStream_t st);

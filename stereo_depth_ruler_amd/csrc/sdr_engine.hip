@@ -169,7 +169,10 @@ int sdr::ensure(Buf& b, size_t bytes) {
     hipError_t e = hipMalloc(&b.p, bytes);
     if (e != hipSuccess) {
         b.p = nullptr;
-        return fail(SDR_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+        const bool cap = e == hipErrorStreamCaptureUnsupported || e == hipErrorStreamCaptureInvalidated;
+        return fail(SDR_ERR_NOMEM, std::string("hipMalloc failed: ") + hipGetErrorString(e) +
+                                       (cap ? " (scratch grows inside a graph capture: make one call of "
+                                              "this shape before capturing)" : ""));
     }
     b.n = bytes;
     return SDR_OK;
@@ -349,11 +352,26 @@ struct sdr_sgbm {
 };
 
 namespace {
+// A stream being captured into a graph (hipStreamBeginCapture, torch.cuda.graph).
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+// The handle's last enqueue, for the next stream that uses its scratch.  Not recorded into a
+// graph capture: the capture's replays order themselves.
 void retire(sdr_sgbm* h) {
-    if (h->done && hipEventRecord(h->done, h->stream) == hipSuccess) h->pending = true;
+    if (!h->done) return;
+    if (capturing(h->stream)) {
+        h->pending = false;
+        return;
+    }
+    if (hipEventRecord(h->done, h->stream) == hipSuccess) h->pending = true;
 }
 int use_stream(sdr_sgbm* h, hipStream_t s) {
-    if (s != h->stream && h->pending) SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
+    // a stream being captured neither queries nor waits on an event recorded outside the capture
+    // (both invalidate a global-mode capture); torch.cuda.graph synchronises before it captures,
+    // and a caller capturing by hand orders the handle's earlier work before the capture itself
+    if (s != h->stream && h->pending && !capturing(s)) SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
     h->stream = s;
     return SDR_OK;
 }
@@ -476,7 +494,9 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     // (when every tile of the frames in flight fits the resident grid); the records are then
     // E, W, up, down -- saturated sums of non-negative path costs, so the grouping is exact
     sdr::SweepShape shp[2] = {};  // [0]: down (SE, SW), [1]: up (N, NE, NW)
-    if (e.mode == SDR_MODE_HH && F >= kSweepMinFrames && g.W1 > 0)
+    // (not inside a graph capture: its replays could overlap another sweep's, which the event
+    // chain below orders for directly enqueued sweeps only)
+    if (e.mode == SDR_MODE_HH && F >= kSweepMinFrames && g.W1 > 0 && !capturing(h->stream))
         for (int up = 0; up < 2; up++) shp[up] = sdr::sweep_shape(g, F, up != 0);
     const bool sweep = shp[0].nslots > 0 && shp[1].nslots > 0;
     const int nrec = sweep ? 4 : P - 1;  // L records per pixel
@@ -494,8 +514,11 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     const size_t slack = (size_t)sdr::kSouthPad * g.W1 * g.D;
     const size_t lslack = slack * nrec;
     const size_t lfs = (size_t)nrec * cells;  // L elements per frame, [H][W1][nrec][D]
+    // a batch that can take the sweep sizes L for the chains' P - 1 records too, so a graph
+    // capture of the same shape (chains only) allocates nothing
+    const size_t lrec = e.mode == SDR_MODE_HH && F >= kSweepMinFrames ? (size_t)(P - 1) : (size_t)nrec;
     if ((rc = ensure(h->C, (F * cells + 2 * slack) * 2))) return rc;
-    if ((rc = ensure(h->Lr, (F * lfs + 2 * lslack) * 2))) return rc;
+    if ((rc = ensure(h->Lr, (F * cells + 2 * slack) * lrec * 2))) return rc;
     if ((rc = ensure(h->keys2, F * px * 4))) return rc;
     // the E/W chains redirected into it (RowRedirect) load up to a lookahead past a row's ends
     const size_t aux_slack = (size_t)sdr::kSouthPad * g.D;

@@ -480,3 +480,36 @@ def test_host_call_refused_before_upload(oracle):
     m.setP2(2400)
     ref = oracle.sgbm_compute(L, R, oracle.make_params(0, 32, 5, 600, 2400, 1, 63, 12, 30, 2, 0))
     assert np.array_equal(m.compute(L, R), ref)
+
+
+def test_graph_capture_replay(oracle):
+    """The device enqueue captured into a graph (torch.cuda.graph: hipStreamBeginCapture on a side
+    stream) and replayed on new inputs: after a first call nothing is allocated, so the launches
+    replay as captured.  Also a batched MODE_HH call, which takes k_paths' chains inside a capture
+    (the row sweeps are not captured)."""
+    dev = torch.device("cuda", 0)
+    for args, F, (H, W, D) in (((0, 64, 5, 600, 2400, 1, 63, 12, 50, 2, 0), 2, (48, 200, 64)),
+                               ((0, 32, 5, 600, 2400, 1, 63, 10, 0, 2, sdr.MODE_HH), 8, (24, 120, 32))):
+        Ls, Rs = S.make_batch(F, H, W, D, seed0=500)
+        Ld, Rd = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+        m = sdr.StereoSGBM.create(*args)
+        m.compute(Ld, Rd)  # sizes the scratch
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = m.compute(Ld, Rd)
+        p = oracle.make_params(*args)
+        for seed in (600, 700):
+            L2, R2 = S.make_batch(F, H, W, D, seed0=seed)
+            Ld.copy_(torch.from_numpy(L2))
+            Rd.copy_(torch.from_numpy(R2))
+            g.replay()
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            for i in range(F):
+                assert np.array_equal(got[i], oracle.sgbm_compute(L2[i], R2[i], p)), (args[10], seed, i)
+        # the handle is still usable directly after the capture
+        again = m.compute(Ld, Rd)
+        torch.cuda.synchronize()
+        assert np.array_equal(again.cpu().numpy(), got)
+        m.close()

@@ -21,9 +21,13 @@ namespace sdr {
 // The window is walked over "virtual" rows q = t-SH2 .. t+SH2 (physical row clamp(q, s0, H-1)),
 // so the ring of the last NR rows is a plain sliding window with compile-time slots.
 // ------------------------------------------------------------------------------------------
-// parity half of a staged R plane: >= ceil(STR/2), == 16 (mod 32) so the even/odd halves of a
-// 32-lane staging store land on disjoint banks
-__host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 15) / 32 * 32 + 16; }
+// parity half of a staged R plane, in 8-byte entries: >= ceil(STR/2) and == 8 (mod 16).  A
+// ds_write_b64 is serviced in 16-lane groups on 32 banks ((a/4) mod 32): the group's 8 even lanes
+// store 64 consecutive bytes into one half and its 8 odd lanes the same bytes of the other, so
+// the halves must sit 64 bytes apart mod 128 to take disjoint banks (at == 16 (mod 32), 128 bytes
+// apart, every staging store was 2-way conflicted: C2 1.07 M conflict cycles a launch).  The
+// reads are ds_read_b64 of 32 consecutive entries, conflict-free at any offset.
+__host__ __device__ inline int cost_half_r(int STR) { return ((STR + 1) / 2 + 7) / 16 * 16 + 8; }
 
 template <int NR, int K, int CN>
 struct CostCfg {

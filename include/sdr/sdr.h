@@ -109,7 +109,10 @@ int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* 
                                size_t xyz_stride);
 
 /* Device-pointer batch compute, asynchronous on the handle's stream: nframes frames spaced
- * frame_stride bytes (inputs) / disp_frame_stride elements (output) apart. */
+ * frame_stride bytes (inputs) / disp_frame_stride elements (output) apart.  Once a call of the
+ * same shape has sized the scratch, the enqueue allocates nothing and may be captured into a
+ * hipGraph on the handle's stream (hipStreamBeginCapture, global mode) and replayed; a captured
+ * batched MODE_HH call takes the per-direction chains instead of the row sweeps. */
 int sdr_sgbm_compute_device(sdr_sgbm* h, const uint8_t* d_left, const uint8_t* d_right,
                             int width, int height, size_t stride, size_t frame_stride,
                             int nframes, int16_t* d_disp, size_t disp_stride,

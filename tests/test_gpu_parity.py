@@ -513,3 +513,30 @@ def test_graph_capture_replay(oracle):
         torch.cuda.synchronize()
         assert np.array_equal(again.cpu().numpy(), got)
         m.close()
+
+
+def test_graph_capture_compute_reproject(oracle):
+    """The fused pcd_write hot path (compute -> /16 -> reprojectImageTo3D with handleMissing, the
+    frame minimum included) captured once and replayed on new frames, bit-exact."""
+    dev = torch.device("cuda", 0)
+    args, (H, W, D) = (0, 64, 5, 600, 2400, 1, 63, 12, 60, 2, 0), (56, 224, 64)
+    L, R, _ = S.make_pair(H, W, D, seed=801)
+    Ld, Rd = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    m = sdr.StereoSGBM.create(*args)
+    m.compute_reproject(Ld, Rd, S.REFERENCE_Q, True)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        disp, xyz = m.compute_reproject(Ld, Rd, S.REFERENCE_Q, True)
+    p = oracle.make_params(*args)
+    for seed in (802, 803):
+        L2, R2, _ = S.make_pair(H, W, D, seed=seed)
+        Ld.copy_(torch.from_numpy(L2))
+        Rd.copy_(torch.from_numpy(R2))
+        g.replay()
+        torch.cuda.synchronize()
+        ref = oracle.sgbm_compute(L2, R2, p)
+        assert np.array_equal(disp[0].cpu().numpy(), ref), seed
+        ref_xyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, True)
+        assert np.array_equal(xyz[0].cpu().numpy().view(np.uint32), ref_xyz.view(np.uint32)), seed
+    m.close()

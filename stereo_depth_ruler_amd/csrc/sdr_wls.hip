@@ -208,12 +208,11 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const f
                 if (k0 + j <= last) fwd(k0 + j, j);
         }
         if (k0 + PF > last) break;
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            r0[j] = n0[j];
-            if constexpr (U1) r1[j] = n1[j];
-            rc[j] = nc[j];
-        }
+        // whole-array copies (register renames after SROA; an element loop here was rewritten
+        // into a copy idiom before the unroller ran, which then warned)
+        __builtin_memcpy(r0, n0, sizeof r0);
+        if constexpr (U1) __builtin_memcpy(r1, n1, sizeof r1);
+        __builtin_memcpy(rc, nc, sizeof rc);
     }
     // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
     if (last < 1) return;

@@ -10,12 +10,19 @@ subpixel, LR check, median 3x3, speckle filter) + convertTo(1/16) + reprojectIma
 Frames shard across ranks (rank r owns its own frame stream); with N > 1 each step's int16
 disparity is gathered to rank 0 over RCCL (the north star's frame-shard + gather).  Rank 0
 prints one JSON line.  value = all ranks' pixels / max-over-ranks wall time.
+
+`--gpus N` with N > 1 and no launcher environment (WORLD_SIZE unset) starts the N ranks itself:
+this process never touches HIP, runs `torch.distributed.run --nproc-per-node N` on this same
+script as a child, relays rank 0's JSON line and exits with the child's status.  Under a
+launcher, WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -177,7 +184,45 @@ def load_traffic(kernel_tag):
         return None
 
 
-def main():
+def free_port() -> int:
+    """A free TCP port on 127.0.0.1 for the ranks' rendezvous."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(nproc: int, port: int, argv) -> list:
+    """torch.distributed.run over this script with the same arguments (one rank per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def relay(cmd, nproc: int, env=None) -> int:
+    """Runs the launcher as a child, passes its output through (stdout line by line, so the
+    driver's progress watch sees it), checks that exactly one JSON line came back and that it
+    reports nproc GPUs, and returns the exit status (the child's, or 3 for a bad line)."""
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, env=env)
+    lines = []
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        s = line.strip()
+        if s.startswith("{") and s.endswith("}"):
+            try:
+                lines.append(json.loads(s))
+            except ValueError:
+                pass
+    rc = p.wait()
+    if rc != 0:
+        log(f"bench: launcher exited with status {rc}")
+        return rc
+    if len(lines) != 1 or lines[0].get("n_gpus") != nproc:
+        log(f"bench: expected one JSON line with n_gpus={nproc}, got {[ln.get('n_gpus') for ln in lines]}")
+        return 3
+    return 0
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -201,12 +246,27 @@ def main():
                          "then, and every rank exits non-zero (RankFailure) instead of blocking")
     ap.add_argument("--inject-failure", default=None, metavar="RANK:STEP",
                     help="test hook: rank RANK's step STEP raises SDR_ERR_ARG (failure-path tests)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    return a
+
+
+def main():
+    a = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        # no launcher: start the N ranks from here, before anything initialises HIP (this process
+        # imports no torch; the ranks are fresh child processes)
+        sys.exit(relay(launcher_cmd(a.gpus, free_port(), sys.argv[1:]), a.gpus))
+    world = int(env_world or "1")
+    if world != a.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}: the launcher and the "
+                         f"arguments disagree on the number of ranks")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gloo = a.dist_backend == "gloo"
@@ -216,13 +276,19 @@ def main():
         # every collective bounded by SDR_DIST_TIMEOUT (default 120 s): a rank that dies outright
         # cannot leave the others blocked (stereo_depth_ruler_amd/distributed.py)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        ndev = torch.cuda.device_count()
         if gloo:
-            local = local % torch.cuda.device_count()
+            local = local % ndev
             torch.cuda.set_device(local)
             init_process_group("gloo")
         else:
+            if ndev < world:
+                raise SystemExit(f"bench: {world} ranks over RCCL need {world} GPUs, this node shows {ndev} "
+                                 f"(--dist-backend gloo rehearses the N>1 path on fewer)")
             torch.cuda.set_device(local)
             init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f"bench: the process group has {dist.get_world_size()} ranks, --gpus {a.gpus}")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -234,7 +300,9 @@ def main():
     KERNEL_KINDS = {"prefilter": _sg.KERNEL_PREFILTER, "k_cost": _sg.KERNEL_COST, "k_paths": _sg.KERNEL_PATHS,
                     "k_south_wta": _sg.KERNEL_WTA_LR, "k_lr_check": _sg.KERNEL_LR_CHECK,
                     "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
-                    "reproject": _sg.KERNEL_REPROJECT, "k_sweep": _sg.KERNEL_SWEEP}
+                    "reproject": _sg.KERNEL_REPROJECT, "k_sweep": _sg.KERNEL_SWEEP,
+                    "k_wls_prep": _sg.KERNEL_WLS_PREP, "fgs_pass": _sg.KERNEL_FGS,
+                    "k_wls_final": _sg.KERNEL_WLS_FINAL}
 
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
     D, mode = args[1], args[10]
@@ -278,7 +346,9 @@ def main():
         ms = [p.matcher() for p in pipes]
         closers = pipes
 
-        def run(j, k, slot):
+        def run(j, k, slot, ingest_events=None):
+            if kind == "live":
+                return pipes[k].enqueue(sbs[j:j + batch], streams[k], ingest_events=ingest_events)
             return pipes[k].enqueue(sbs[j:j + batch], streams[k])
     m = ms[0]
     gather_bufs = None
@@ -353,10 +423,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    ranks = None
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cpu" if gloo else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        # every rank's own wall time (host-side exchange), then the max over ranks
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "device": dev.index, "host": socket.gethostname(),
+                                          "ms_per_step": round(el / a.steps * 1e3, 4), "_s": el})
+        el = max(r.pop("_s") for r in per_rank)
+        ranks = {"backend": "gloo" if gloo else "nccl (RCCL)", "world_size_seen": dist.get_world_size(),
+                 "per_rank": per_rank}
     gather_check = None
     if world > 1:
         # end-to-end check of the data path (after the timed region): rank 0's copy of every rank's
@@ -374,13 +449,21 @@ def main():
 
     Wm, Hm = (W // 2, H // 2) if kind == "live" else (W, H)  # the left matcher's frame
     w1 = Wm - max(args[0] + D, 0) + min(args[0], 0)
-    cells = batch * Hm * w1 * D
+    # the class path (live) runs the left and the right matcher as one paired batch through the
+    # same launches (stereo_disparity.cpp:27-28); the right one (minD = -(minD + D) + 1) matches
+    # the same W1 columns
+    nmatch = 2 if kind == "live" else 1
+    cells = nmatch * batch * Hm * w1 * D
     P = NPATHS[mode]
 
-    def kernel_report(mm):
-        """Per-kernel HIP-event times of matcher mm since its last reset -> (kernels, roofline)."""
+    def kernel_report(mm, extra=None):
+        """Per-kernel HIP-event times of matcher mm since its last reset -> (kernels, roofline).
+        extra: {name: (total_ms, launches)} of launches timed outside the handle (the ingest)."""
         per_kind = {name: mm.kernel_time(kind, reset=False) for name, kind in KERNEL_KINDS.items()}
         all_ms, _ = mm.kernel_time(-1, reset=True)
+        for name, v in (extra or {}).items():
+            per_kind[name] = v
+            all_ms += v[0]
         kern = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
                        "share": round(ms / all_ms, 4) if all_ms else None}
                 for name, (ms, c) in per_kind.items() if c}
@@ -422,7 +505,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": load_traffic(f"{a.config}:{name}"),
             "algorithmic_bytes_per_launch": bytes_per_launch,
-            "bytes_model": f"{model}; cells=batch*H*W1*D={cells}",
+            "bytes_model": f"{model}; cells={'2 matchers*' if nmatch == 2 else ''}batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),
             "launches_timed": cnt,
             "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
@@ -456,12 +539,19 @@ def main():
         torch.cuda.synchronize()
         m.enable_timing(2)
         m.kernel_time(-1, reset=True)
+        ingest = []
         with torch.cuda.stream(streams[0]):
             for i in range(max(1, a.iso_steps)):
                 j = (i * batch) % (nf - batch + 1) if nf > batch else 0
-                run(j, 0, 0)
+                if kind == "live":  # k_sbs_ingest runs on the rectifier's handle: torch events
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ingest.append(ev)
+                    run(j, 0, 0, ingest_events=ev)
+                else:
+                    run(j, 0, 0)
         torch.cuda.synchronize()
-        kernels, roofline = kernel_report(m)
+        extra = {"k_sbs_ingest": (sum(e0.elapsed_time(e1) for e0, e1 in ingest), len(ingest))} if ingest else None
+        kernels, roofline = kernel_report(m, extra)
         if roofline is not None:
             roofline["measured"] = (f"HIP events around each launch, {max(1, a.iso_steps)} single-stream steps "
                                     f"after the timed region")
@@ -473,7 +563,7 @@ def main():
     value = pix / el / 1e6
     if roofline is not None:
         # B_frame = cells*(2+6P) + 16 B/px, times the whole job's frame rate
-        b_frame = cells * (2 + 6 * P) + 16 * Hm * Wm * batch
+        b_frame = cells * (2 + 6 * P) + 16 * Hm * Wm * batch * nmatch
         job = b_frame * world * a.steps / el / 1e9
         roofline["job"] = {"model_bytes_per_step": b_frame, "achieved": round(job, 1),
                            "frac": round(job / HBM_PEAK_GBS / world, 4),
@@ -505,6 +595,7 @@ def main():
             "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),
+        "ranks": ranks,
         "gather_check": gather_check,
         "roofline": roofline,
         "kernels": kernels,

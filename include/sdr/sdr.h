@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define SDR_ABI_VERSION 3
+#define SDR_ABI_VERSION 4
 
 /* cv::StereoSGBM::MODE_* */
 enum { SDR_MODE_SGBM = 0, SDR_MODE_HH = 1, SDR_MODE_SGBM_3WAY = 2, SDR_MODE_HH4 = 3 };
@@ -379,11 +379,29 @@ enum {
     SDR_KERNEL_WTA_LR = 3,   /* k_south_wta: top-to-bottom path fused with WTA/uniqueness/disp2 */
     SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6,
     SDR_KERNEL_LR_CHECK = 7, /* the LR-checked map materialised (debug stage 2 only since round 3) */
-    SDR_KERNEL_SWEEP = 8     /* k_sweep: batched MODE_HH's up (N, NE, NW) and down (SE, SW) passes */
+    SDR_KERNEL_SWEEP = 8,    /* k_sweep: batched MODE_HH's up (N, NE, NW) and down (SE, SW) passes */
+    /* the class path's WLS filter (sdr_stereo_class_*), recorded on the left matcher's handle */
+    SDR_KERNEL_WLS_PREP = 9, /* k_wls_prep (or k_wls_disc + k_wls_conf past 4096 ROI columns) */
+    SDR_KERNEL_FGS = 10,     /* one FGS pass: k_fgs_pcr, or k_fgs_sweep (+ its transposes) */
+    SDR_KERNEL_WLS_FINAL = 11 /* k_wls_final (+ /16 + computeDepth epilogue) */
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);
 int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int* count);
+
+/* Status of the handle's device batches since the last report (synchronises the handle's
+ * stream).  A batched MODE_HH call (>= 8 frames, sdr_sgbm_compute_device*) runs row sweeps whose
+ * workgroups wait on their neighbours; they assume every workgroup of the sweep is resident, i.e.
+ * that this process has the device to itself (sweeps of one process are ordered among themselves).
+ * If a wait still gives up (another process's persistent kernel holding CUs for about a second),
+ * that batch's output frames are written as INVALID ((minDisparity-1)*16, the reprojection's
+ * frame minima too) and this call returns SDR_ERR_DEVICE once, then SDR_OK again.  The
+ * host-pointer entry points compute one frame and never take the sweeps. */
+int sdr_sgbm_last_status(sdr_sgbm* h);
+/* Test hooks.  SDR_DEBUG_SWEEP_SPIN: polls a sweep's neighbour wait makes before it gives up
+ * (<= 0: the default, about a second); a small value forces the failure path above. */
+enum { SDR_DEBUG_SWEEP_SPIN = 1 };
+int sdr_sgbm_debug_knob(sdr_sgbm* h, int knob, int value);
 
 /* Device self-test of the cross-lane primitives the kernels rely on (DPP wave shifts,
  * permlane swaps); fills 4 failure counters, all zero on a healthy gfx950. */
@@ -408,6 +426,9 @@ int sdr_host_free(void* p);
 
 const char* sdr_last_error(void);
 int sdr_abi_version(void);
+/* Hash of the sources the library was built from (stereo_depth_ruler_amd/build.py source_hash):
+ * the build and the smoke test compare it with the tree's sources. */
+const char* sdr_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -153,6 +153,9 @@ SIGNATURES = [
     ("sdr_selftest_wave_ops", _i, [_c.POINTER(_c.c_int)]),
     ("sdr_sgbm_debug_stage", _i, [_vp, _i, _vp, _sz]),
     ("sdr_sgbm_kernel_time", _i, [_vp, _i, _i, _c.POINTER(_c.c_float), _c.POINTER(_c.c_int)]),
+    ("sdr_sgbm_last_status", _i, [_vp]),
+    ("sdr_sgbm_debug_knob", _i, [_vp, _i, _i]),
+    ("sdr_build_id", _c.c_char_p, []),
     ("sdr_last_error", _c.c_char_p, []),
     ("sdr_abi_version", _i, []),
 ]

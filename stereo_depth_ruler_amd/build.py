@@ -5,6 +5,7 @@ It is built here (cross-compiled, no GPU needed) and travels to the GPU box with
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -26,13 +27,41 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm is required to build the engine)")
 
 
+def _deps():
+    return [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "sdr", "sdr.h")]
+
+
+def _hash(paths, extra=()) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    for x in extra:
+        h.update(str(x).encode() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def source_hash() -> str:
+    """Hash of every source, header and the ABI header the library is built from, and the target
+    arch: the library embeds it (sdr_build_id) and a build is stale exactly when it differs."""
+    return _hash(_deps(), (ARCH,))
+
+
+def built_id(path: str = OUT):
+    """The build id embedded in a built library, or None."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(b"SDR_BUILD_ID=")
+    return data[i + 13:i + 29].decode(errors="replace") if i >= 0 else None
+
+
 def _stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps.append(os.path.join(ROOT, "include", "sdr", "sdr.h"))
-    return any(os.path.getmtime(d) > t for d in deps)
+    return built_id() != source_hash()
 
 
 # host-only debug info: device debug info of the unrolled cost kernels takes hipcc tens of minutes
@@ -57,21 +86,34 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
              "-I", os.path.join(ROOT, "include")] + [f"-D{d}" for d in defines] + list(extra)
     hipcc = _hipcc()
     objs, procs = [], []
-    hdr_t = max(os.path.getmtime(d) for d in [os.path.join(CSRC, h) for h in HEADERS] +
-                [os.path.join(ROOT, "include", "sdr", "sdr.h")])
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "sdr", "sdr.h")]
     for f in SOURCES:
         obj = os.path.join(objdir, f.replace(".hip", ".o"))
         objs.append(obj)
-        # an object newer than its source and every header is reused (same flags: one objdir per variant)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, f))):
+        # an object is reused when its recorded hash (source, headers, flags) still matches
+        key = _hash([os.path.join(CSRC, f)] + hdrs, flags)
+        stamp = obj + ".hash"
+        if not force and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
             continue
         cmd = [hipcc, *flags, "-c", os.path.join(CSRC, f), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        procs.append((cmd, subprocess.Popen(cmd)))
-    failed = [cmd for cmd, p in procs if p.wait() != 0]
+        procs.append((cmd, subprocess.Popen(cmd), stamp, key))
+    failed = [cmd for cmd, p, _, _ in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
+    for _, _, stamp, key in procs:
+        with open(stamp, "w") as fh:
+            fh.write(key)
+    # the build id: the hash of the sources this library is linked from (sdr_build_id)
+    bid_src = os.path.join(objdir, "sdr_build_id.cpp")
+    with open(bid_src, "w") as fh:
+        fh.write('extern "C" const char* sdr_build_id(void) {\n'
+                 f'    static const char id[] = "SDR_BUILD_ID={source_hash()}";\n'
+                 '    return id + 13;\n}\n')
+    bid_obj = os.path.join(objdir, "sdr_build_id.o")
+    subprocess.check_call([hipcc, "-O2", "-fPIC", "-x", "c++", "-c", bid_src, "-o", bid_obj])
+    objs.append(bid_obj)
     link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *extra, *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(link))

@@ -323,10 +323,13 @@ struct sdr_sgbm {
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
     Buf planesL, planesR, sink, C, Lr, Caux, draw, dlr, dfin, labels, sizes, mins, hin, hxyz, keys2;
-    // MODE_HH row sweeps: [2 passes][slots][tiles][2] counters, the error word, the edge rings;
-    // sweep_err_host: the error word of the last sweep, copied back asynchronously (page-locked)
-    Buf sweep;
-    int* sweep_err_host = nullptr;
+    // MODE_HH row sweeps: [2 passes][slots][tiles][2] counters, the call's error word, the edge
+    // rings.  status: the handle's sticky status word on the device (set by a batch whose sweep
+    // wait timed out, never cleared by a call; sdr_sgbm_last_status reports and clears it),
+    // status_host: its page-locked copy, refreshed after every sweep batch
+    Buf sweep, status;
+    int* status_host = nullptr;
+    int sweep_spin = sdr::kSweepSpin;  // debug knob SDR_DEBUG_SWEEP_SPIN
     HostXfer hx;  // pinned staging of the host-pointer entry points
     Buf cls_bgr, cls_gray, cls_small, cls_dl, cls_wls, cls_f, cls_conf, cls_filt;
     int timing = 0;  // 0 off, 1 stage events, 2 stage + per-kernel events
@@ -377,29 +380,32 @@ int use_stream(sdr_sgbm* h, hipStream_t s) {
 }
 }  // namespace
 
+bool sdr::ktimer_begin(sdr_sgbm* h, int kind) {
+    if (h->timing < 2) return false;
+    if (h->kused * 2 + 2 > h->kev.size()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreate(&a) != hipSuccess) return false;
+        if (hipEventCreate(&b) != hipSuccess) {
+            (void)hipEventDestroy(a);
+            return false;
+        }
+        h->kev.push_back(a);
+        h->kev.push_back(b);
+        h->kkind.push_back(kind);
+    }
+    h->kkind[h->kused] = kind;
+    (void)hipEventRecord(h->kev[2 * h->kused], h->stream);
+    return true;
+}
+
+void sdr::ktimer_end(sdr_sgbm* h) {
+    (void)hipEventRecord(h->kev[2 * h->kused + 1], h->stream);
+    h->kused++;
+}
+
 namespace {
 // RAII event pair around one kernel launch when per-kernel timing is on.
-struct KTimer {
-    sdr_sgbm* h;
-    bool on;
-    KTimer(sdr_sgbm* h_, int kind) : h(h_), on(h_->timing >= 2) {
-        if (!on) return;
-        if (h->kused * 2 + 2 > h->kev.size()) {
-            hipEvent_t a = nullptr, b = nullptr;
-            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
-            h->kev.push_back(a);
-            h->kev.push_back(b);
-            h->kkind.push_back(kind);
-        }
-        h->kkind[h->kused] = kind;
-        (void)hipEventRecord(h->kev[2 * h->kused], h->stream);
-    }
-    ~KTimer() {
-        if (!on) return;
-        (void)hipEventRecord(h->kev[2 * h->kused + 1], h->stream);
-        h->kused++;
-    }
-};
+using KTimer = sdr::KScope;
 }  // namespace
 
 
@@ -484,10 +490,6 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     }
     if ((rc = check_frame(e))) return rc;
 
-    // a failed neighbour wait of an earlier call's MODE_HH sweep (its error word, copied back
-    // after that launch) is reported now: the frames it produced were wrong
-    if (h->sweep_err_host && __atomic_exchange_n(h->sweep_err_host, 0, __ATOMIC_RELAXED))
-        return fail(SDR_ERR_DEVICE, "a MODE_HH row sweep of an earlier call timed out waiting for a tile");
     const size_t cells = (size_t)H * g.W1 * g.D;
     const int P = npaths_of(e.mode);
     // batched MODE_HH: N/NE/NW and SE/SW as two row-synchronous sweeps into one record each
@@ -546,9 +548,14 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     const size_t sweep_flags = (flags_n[0] + flags_n[1]) * sizeof(int);
     if (sweep) {
         if ((rc = ensure(h->sweep, sweep_flags + 256 + edge_bytes))) return rc;
-        if (!h->sweep_err_host && hipHostMalloc((void**)&h->sweep_err_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
-            h->sweep_err_host = nullptr;
-            return fail(SDR_ERR_NOMEM, "hipHostMalloc failed");
+        if (!h->status_host) {
+            if ((rc = ensure(h->status, 256))) return rc;
+            SDR_HIP(hipMemsetAsync(h->status.p, 0, 256, st));
+            if (hipHostMalloc((void**)&h->status_host, sizeof(int), hipHostMallocDefault) != hipSuccess) {
+                h->status_host = nullptr;
+                return fail(SDR_ERR_NOMEM, "hipHostMalloc failed");
+            }
+            *h->status_host = 0;
         }
     }
     int16_t* draw = (int16_t*)h->draw.p;
@@ -689,6 +696,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         sa.flags = (int*)sb;
         sa.err = (int*)(sb + sweep_flags);
         sa.edge = (uint32_t*)(sb + sweep_flags + 256);
+        sa.spin = h->sweep_spin;
         std::lock_guard<std::mutex> lk(g_sweep_mu);
         hipEvent_t& last = g_sweep_last[h->device];
         if (last) SDR_HIP(hipStreamWaitEvent(st, last, 0));
@@ -703,7 +711,6 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             sa.flags += flags_n[up];
         }
         SDR_HIP(hipEventRecord(last, st));
-        SDR_HIP(hipMemcpyAsync(h->sweep_err_host, sb + sweep_flags, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
@@ -733,6 +740,13 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             KTimer kt(h, SDR_KERNEL_REPROJECT);
             sdr::launch_min_s16(dst, px, px, F, out_min, st);
         }
+    }
+    if (sweep) {
+        // a timed-out wait made this batch's frames wrong: they become INVALID (and the handle's
+        // status says so) before anything downstream reads them
+        sdr::launch_sweep_verdict((const int*)((char*)h->sweep.p + sweep_flags), dst, px, F,
+                                  (int16_t)e.invalid, out_min, (int*)h->status.p, st);
+        SDR_HIP(hipMemcpyAsync(h->status_host, h->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
     retire(h);
@@ -801,8 +815,8 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    if (h->sweep_err_host) (void)hipHostFree(h->sweep_err_host);
-    for (Buf* b : {&h->sweep, &h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
+    if (h->status_host) (void)hipHostFree(h->status_host);
+    for (Buf* b : {&h->sweep, &h->status, &h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hxyz, &h->cls_bgr,
                    &h->cls_gray, &h->cls_small, &h->cls_dl, &h->cls_wls, &h->cls_f,
                    &h->cls_conf, &h->cls_filt})
@@ -1239,7 +1253,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         // with filtered_disp.convertTo(CV_32F, 1/16) (:34) and computeDepth (:76-80) in its epilogue
         void* ws = sdr_wls_get_stream(wls);
         (void)sdr_wls_set_stream(wls, st);
-        rc = sdr::wls_filter_enqueue(wls, dl, dr, sl, w2, h2, w2, px2, F, dw, d_conf, d_out, Q, d_xyz);
+        rc = sdr::wls_filter_enqueue(wls, dl, dr, sl, w2, h2, w2, px2, F, dw, d_conf, d_out, Q, d_xyz, left);
         (void)sdr_wls_set_stream(wls, ws);
         if (rc) return rc;
     } else {
@@ -1337,6 +1351,27 @@ int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int*
     if (total_ms) *total_ms = tot;
     if (count) *count = n;
     if (reset) h->kused = 0;
+    return SDR_OK;
+}
+
+int sdr_sgbm_last_status(sdr_sgbm* h) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    if (!h->status_host) return SDR_OK;  // no sweep batch has run on this handle
+    SDR_HIP(hipSetDevice(h->device));
+    SDR_HIP(hipStreamSynchronize(h->stream));
+    if (!__atomic_load_n(h->status_host, __ATOMIC_ACQUIRE)) return SDR_OK;
+    // reported: clear the device word and its copy
+    SDR_HIP(hipMemsetAsync(h->status.p, 0, sizeof(int), h->stream));
+    SDR_HIP(hipStreamSynchronize(h->stream));
+    __atomic_store_n(h->status_host, 0, __ATOMIC_RELEASE);
+    return fail(SDR_ERR_DEVICE, "a MODE_HH row sweep timed out waiting for a neighbouring tile: that "
+                                "batch's frames were written as INVALID");
+}
+
+int sdr_sgbm_debug_knob(sdr_sgbm* h, int knob, int value) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    if (knob != SDR_DEBUG_SWEEP_SPIN) return fail(SDR_ERR_ARG, "unknown knob");
+    h->sweep_spin = value > 0 ? value : sdr::kSweepSpin;
     return SDR_OK;
 }
 

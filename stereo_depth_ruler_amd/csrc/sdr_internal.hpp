@@ -159,7 +159,15 @@ struct SweepArgs {
     int* err;              // set when a neighbour wait times out (never, with every tile resident)
     int ntiles, nslots;    // frames in flight = nslots (workgroups = nslots * ntiles, all resident)
     int up;
+    int spin;              // polls before a wait gives up (kSweepSpin; lower through a debug knob)
 };
+constexpr int kSweepSpin = 1 << 20;  // polls (~1 us each) before a sweep's wait gives up
+// After a batch's sweeps and post-filter: when a wait of this call's sweeps timed out (*err), the
+// batch's frames are wrong, so every pixel of disp [F][n] becomes `invalid`, the reprojection's
+// frame minima too (mins: [F][kMinSlots], nullable), and the handle's sticky status word is set
+// (sdr_sgbm_last_status reports it).  Nothing happens otherwise.
+void launch_sweep_verdict(const int* err, int16_t* disp, size_t n, int F, int16_t invalid, int* mins,
+                          int* sticky, hipStream_t st);
 // a pass's tiling: columns per wave, tiles per frame, frames in flight (slots; 0: the frame's
 // tiles do not fit the resident grid)
 struct SweepShape {
@@ -263,10 +271,24 @@ void launch_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* 
                       size_t dstride, int F, hipStream_t st);
 int selftest_wave_ops(int* failures);
 
+// Per-kernel HIP-event timing of a matcher handle (timing level 2, sdr_sgbm_kernel_time): an
+// event pair of SDR_KERNEL_* kind `kind` on the handle's stream around one launch.  Kernels another
+// file launches for the handle (the class path's WLS filter) bracket themselves with a KScope.
+bool ktimer_begin(sdr_sgbm* h, int kind);  // false: timing is off (and no end follows)
+void ktimer_end(sdr_sgbm* h);
+struct KScope {
+    sdr_sgbm* h;
+    KScope(sdr_sgbm* h_, int kind) : h(h_ && ktimer_begin(h_, kind) ? h_ : nullptr) {}
+    ~KScope() {
+        if (h) ktimer_end(h);
+    }
+};
+
 // DisparityWLSFilter::filter on device (sdr_wls.hip) with the class path's fused epilogue:
-// fout (nullable) = out / 16, xyz (nullable, needs fout and Q) = reprojectImageTo3D(fout, Q)
+// fout (nullable) = out / 16, xyz (nullable, needs fout and Q) = reprojectImageTo3D(fout, Q);
+// timer (nullable): the matcher handle whose per-kernel timing records the filter's launches
 int wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide, int W,
                        int H, size_t gstride, size_t gfstride, int F, int16_t* out, float* conf,
-                       float* fout, const double* Q, float* xyz);
+                       float* fout, const double* Q, float* xyz, sdr_sgbm* timer = nullptr);
 
 }  // namespace sdr

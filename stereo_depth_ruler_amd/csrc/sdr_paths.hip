@@ -233,12 +233,14 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
 // publish their boundary columns' path costs through a global ring (system-coherent sc1 stores,
 // then a row counter; the reader polls the counter).  Every tile of a frame in flight must be
 // resident (sweep_shape sizes the grid from the occupancy; the engine never has two sweeps in
-// flight), and a wait gives up after kSweepSpin polls with *err set.
+// flight), and a wait gives up after a.spin polls with *err set: the batch's frames are then
+// overwritten as INVALID after the post-filter (launch_sweep_verdict) and the handle's status
+// reports SDR_ERR_DEVICE.  Residency assumes this process has the device to itself: another
+// process's persistent kernel holding CUs for longer than the spin budget makes the wait give up.
 // Bytes per cell: one C read (+ 2 / kSweepOwn for the halos) and one record write for
 // the pass (k_paths: one of each per direction); the fused WTA pass then reads one record for
 // them instead of one per direction.
 // ------------------------------------------------------------------------------------------
-constexpr int kSweepSpin = 1 << 20;  // polls (~1 us each) before a wait gives up
 
 // path_step's delta (wave minimum + P2, both halves) of a path-cost vector
 template <int K>
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
         while (!gave_up &&
                __builtin_amdgcn_readfirstlane(__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
                    target) {
-            if (++n > kSweepSpin) {
+            if (++n > a.spin) {
                 if (lane == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 gave_up = true;
             }
@@ -515,6 +517,23 @@ SweepShape sweep_shape(const Geometry& g, int F, bool up) {
     sh.ntiles = (g.W1 + tile - 1) / tile;
     sh.nslots = min(F, cus * occ / sh.ntiles);
     return sh;
+}
+
+__global__ __launch_bounds__(256) void k_sweep_verdict(const int* __restrict__ err, int16_t* __restrict__ disp,
+                                                       size_t n, int F, int16_t invalid, int* __restrict__ mins,
+                                                       int* __restrict__ sticky) {
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+        return;
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = tid; i < n * F; i += nth) disp[i] = invalid;
+    if (mins)
+        for (size_t i = tid; i < (size_t)F * kMinSlots; i += nth) mins[i] = invalid;
+    if (tid == 0) atomicOr(sticky, 1);
+}
+
+void launch_sweep_verdict(const int* err, int16_t* disp, size_t n, int F, int16_t invalid, int* mins,
+                          int* sticky, hipStream_t st) {
+    hipLaunchKernelGGL(k_sweep_verdict, dim3(1024), dim3(256), 0, st, err, disp, n, F, invalid, mins, sticky);
 }
 
 void launch_sweep(const Geometry& g, const SweepArgs& a, int F, hipStream_t st) {

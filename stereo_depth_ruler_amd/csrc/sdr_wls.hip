@@ -279,20 +279,24 @@ __global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const f
 // images (Ch for rows, Cv for columns, 0 on each line's last sample).
 constexpr int kPcrMaxN = 4096;  // samples per block (G * n): 4 equations per thread of 1024
 
-template <int EPT, bool TWO>
+// DB: the stage buffers double-buffered (48 B of LDS per sample, one barrier per stage), or single
+// (24 B per sample, two barriers per stage) for blocks whose 48 B per sample exceed the
+// workgroup's LDS (160 KiB on gfx950: past 3413 samples)
+template <int EPT, bool TWO, bool DB = true>
 __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const float* __restrict__ Cw,
                                                   int w, int h, size_t fstride, int rows, int G,
                                                   float lam) {
     extern __shared__ float4 pcr_smem[];
+    constexpr int NB = DB ? 2 : 1;
     const int T = blockDim.x;
     const int n = rows ? w : h;
     const int nlines = rows ? h : w;
     const int N = G * n;
-    // two stage buffers: X [2][N] {row sum, 1/b, d0, d1}, then A [2][N] (a; the weights during
-    // the load), Cc [2][N] (c)
+    // NB stage buffers: X [NB][N] {row sum, 1/b, d0, d1}, then A [NB][N] (a; the weights during
+    // the load), Cc [NB][N] (c)
     float4* X = pcr_smem;
-    float* A = (float*)(X + 2 * N);
-    float* Cc = A + 2 * N;
+    float* A = (float*)(X + NB * N);
+    float* Cc = A + NB * N;
     const int tid = threadIdx.x;
     // consecutive line groups share an XCD: the column pass's G-column blocks of one row band
     // read and write parts of the same cache lines, which then meet in one L2
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
     }
     __syncthreads();
     int buf = 0;
-    for (int s = 1; s < n; s <<= 1, buf ^= N) {
+    for (int s = 1; s < n; s <<= 1, buf ^= DB ? N : 0) {
         float4* Xb = X + buf;
         float* Ab = A + buf;
         float* Cb = Cc + buf;
@@ -393,6 +397,7 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
                 if constexpr (TWO) d1[j] = (d1[j] - xm.w * k1) - xp.w * k2;
             }
         }
+        if constexpr (!DB) __syncthreads();  // every read of the one buffer done before the next writes
     }
     // ---- decoupled: u = d / b, staged in LDS (buffer `buf`, untouched since two stages back) for
     // the coalesced store ----
@@ -637,8 +642,24 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
     const int ept = N <= 1024 ? 1 : N <= 2048 ? 2 : 4;
     const int T = std::min(1024, ((N + ept - 1) / ept + 63) / 64 * 64);
     const dim3 grid((nlines + G - 1) / G, F), blk(T);
-    const size_t lds = (size_t)N * 48;
     const size_t fs = (size_t)w * h;
+    // the workgroup's LDS (160 KiB on gfx950) holds double-buffered stages up to 3413 samples
+    static thread_local int max_lds = 0;
+    if (!max_lds) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+            max_lds <= 0)
+            max_lds = 64 * 1024;
+    }
+    const bool db = (size_t)N * 48 <= (size_t)max_lds;
+    if (!db && (size_t)N * 24 > (size_t)max_lds) return -1;
+    if (!db) {
+        hipLaunchKernelGGL((k_fgs_pcr<4, TWO, false>), grid, blk, (size_t)N * 24, st, U0, U1, Cw, w, h, fs, rows,
+                           G, lam);
+        return 0;
+    }
+    const size_t lds = (size_t)N * 48;
     if (ept == 1) hipLaunchKernelGGL((k_fgs_pcr<1, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
     else if (ept == 2) hipLaunchKernelGGL((k_fgs_pcr<2, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
     else hipLaunchKernelGGL((k_fgs_pcr<4, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
@@ -655,7 +676,7 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
 static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
                       int iters, int solver, const FgsScratch& s, hipStream_t st,
-                      bool weights_ready = false) {
+                      bool weights_ready = false, sdr_sgbm* timer = nullptr) {
     const size_t fs = (size_t)w * h;
     const bool pcr = solver == SDR_FGS_PCR;
     if (!weights_ready)
@@ -666,17 +687,28 @@ static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, con
     const float fa = (float)att;
     for (int it = 0; it < iters; it++) {
         if (pcr) {
-            const int e1 = R1 ? launch_pcr<true>(R0, R1, s.ChT, w, h, F, 1, lam, st)
-                              : launch_pcr<false>(R0, R1, s.ChT, w, h, F, 1, lam, st);
-            const int e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
-                              : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
+            int e1, e2;
+            {
+                KScope kt(timer, SDR_KERNEL_FGS);
+                e1 = R1 ? launch_pcr<true>(R0, R1, s.ChT, w, h, F, 1, lam, st)
+                        : launch_pcr<false>(R0, R1, s.ChT, w, h, F, 1, lam, st);
+            }
+            {
+                KScope kt(timer, SDR_KERNEL_FGS);
+                e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
+                        : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
+            }
             if (e1 || e2) return -1;
         } else {
-            // row pass on column-major copies (lines = rows, k = column)
-            hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
-            fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
-            hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
+            {
+                // row pass on column-major copies (lines = rows, k = column)
+                KScope kt(timer, SDR_KERNEL_FGS);
+                hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
+                fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
+                hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
+            }
             // column pass in place on the row-major images (lines = columns, k = row)
+            KScope kt(timer, SDR_KERNEL_FGS);
             fgs_sweep(dim3((w + 63) / 64, F), st, R0, R1, s.Cv, s.T, w, h, fs, lam);
         }
         lam = lam * fa;  // FastGlobalSmootherFilterImpl::filter: lambda *= lambda_attenuation
@@ -841,7 +873,7 @@ int sdr_wls_get_roi(const sdr_wls* h, int W, int H, int roi[4]) {
 // k_fgs_weights kernels.
 int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8_t* guide,
                             int W, int H, size_t gstride, size_t gfstride, int F, int16_t* out,
-                            float* conf, float* fout, const double* Q, float* xyz) {
+                            float* conf, float* fout, const double* Q, float* xyz, sdr_sgbm* timer) {
     if (!h || !dl || !dr || !guide || !out) return sdr::set_error(SDR_ERR_ARG, "null argument");
     if (W <= 0 || H <= 0 || F <= 0 || gstride < (size_t)W || (F > 1 && gfstride < gstride * H))
         return sdr::set_error(SDR_ERR_ARG, "bad size/stride");
@@ -885,10 +917,12 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     const bool rowmajor = p.fgs_solver == SDR_FGS_PCR;
     const dim3 grid((W + 63) / 64, (H + 3) / 4, F);
     if (fused) {
+        sdr::KScope kt(timer, SDR_KERNEL_WLS_PREP);
         hipLaunchKernelGGL(sdr::k_wls_prep, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
                            gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
                            (float*)h->Cv.p);
     } else {
+        sdr::KScope kt(timer, SDR_KERNEL_WLS_PREP);
         if (roi)
             hipLaunchKernelGGL(sdr::k_wls_disc, dim3((g.rw + 63) / 64, (g.rh + 3) / 4, F), blk, 0, st,
                                dr, g, (float*)h->rdisc.p);
@@ -900,14 +934,17 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
         const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
                                  (float*)h->Cv.p};
         if (sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
-                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused))
+                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused, timer))
             return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                                 "(use SDR_FGS_THOMAS for larger ROIs)");
     }
     sdr::Q16 q{};
     if (Q)
         for (int t = 0; t < 16; t++) q.q[t] = Q[t];
-    hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out, fout, q, xyz);
+    {
+        sdr::KScope kt(timer, SDR_KERNEL_WLS_FINAL);
+        hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out, fout, q, xyz);
+    }
     WLS_HIP(hipGetLastError());
     return SDR_OK;
 }

@@ -62,15 +62,21 @@ def error_code(err) -> int:
 
 
 def check_ranks(code: int = 0, group=None) -> None:
-    """All ranks exchange their status (0 = ok); raises RankFailure on every rank if any is not 0.
-    Host-side (gloo), so it never waits on a GPU stream."""
+    """All ranks of `group` (default: the world) exchange their status (0 = ok); raises
+    RankFailure on every rank if any is not 0.  Over the host-side gloo status group when the world
+    is meant (it never waits on a GPU stream); over `group` itself otherwise, with the codes in
+    device memory when that group's backend is nccl (RCCL has no host tensors).  A world set up
+    by torch.distributed.init_process_group directly (no status group) is treated the same way."""
     import torch
     import torch.distributed as dist
 
     g = group if group is not None else _status_group
+    dev = "cpu"
+    if dist.get_backend(g) != "gloo":
+        dev = torch.device("cuda", torch.cuda.current_device())
     world = dist.get_world_size(g)
-    mine = torch.tensor([int(code)], dtype=torch.int64)
-    codes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    mine = torch.tensor([int(code)], dtype=torch.int64, device=dev)
+    codes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(codes, mine, group=g)
     vals = [int(c.item()) for c in codes]
     if any(vals):
@@ -100,7 +106,7 @@ def gather_frames(local, n_frames: int, world: int, rank: int, group=None, error
     import torch.distributed as dist
 
     try:
-        check_ranks(error_code(error))
+        check_ranks(error_code(error), group=group)
     except RankFailure as f:
         if error is not None:
             raise f from error

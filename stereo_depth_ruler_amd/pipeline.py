@@ -62,15 +62,21 @@ class LiveLoop:
     def matcher(self):
         return self.left
 
-    def enqueue(self, sbs, stream):
-        """sbs: uint8 (batch, H, 2W, 3) on the device; everything runs on `stream`."""
+    def enqueue(self, sbs, stream, ingest_events=None):
+        """sbs: uint8 (batch, H, 2W, 3) on the device; everything runs on `stream`.
+        ingest_events (optional): two torch.cuda.Event recorded on `stream` around the ingest
+        (split + rectify + gray + INTER_AREA), for per-kernel timing."""
         s = _vp(stream.cuda_stream)
         L = lib()
         check(L.sdr_rectifier_set_stream(self.rect._h, s))
         disp_on = self.display is not None
+        if ingest_events:
+            ingest_events[0].record(stream)
         check(L.sdr_rectify_sbs_device(self.rect._h, sbs.data_ptr(), self.W * 6, self.W * 6 * self.H,
                                        self.batch, self.left_rect.data_ptr() if disp_on else None, None,
                                        self.small_l.data_ptr(), self.small_r.data_ptr()))
+        if ingest_events:
+            ingest_events[1].record(stream)
         check(L.sdr_sgbm_set_stream(self.left._h, s))
         # computeDisparity + computeDepth: reprojectImageTo3D(half-res disparity, full-res Q)
         # (stereo_disparity.cpp:76-80), fused into the WLS filter's epilogue

@@ -32,7 +32,8 @@ MODE_SGBM, MODE_HH, MODE_SGBM_3WAY, MODE_HH4 = 0, 1, 2, 3
 UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
 # SDR_KERNEL_* (include/sdr/sdr.h)
 (KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATHS, KERNEL_WTA_LR, KERNEL_MEDIAN, KERNEL_SPECKLE,
- KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP) = range(9)
+ KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP, KERNEL_WLS_PREP, KERNEL_FGS, KERNEL_WLS_FINAL) = range(12)
+DEBUG_SWEEP_SPIN = 1  # sdr_sgbm_debug_knob
 
 
 def _is_cuda(x) -> bool:
@@ -245,6 +246,16 @@ class StereoSGBM:
     def debug_cost_volume(self, H: int, W1: int, D: int) -> np.ndarray:
         """The first frame's cost volume C of the last compute as (H, W1, D) int16."""
         return self.debug_stage(0, (H, W1, D), np.int16)
+
+    def check_status(self):
+        """Raises SDRError(SDR_ERR_DEVICE) if a device batch since the last check had a row sweep
+        give up waiting (its frames were written as INVALID; sdr_sgbm_last_status).  Synchronises
+        the handle's stream."""
+        check(lib().sdr_sgbm_last_status(self._h))
+
+    def set_debug_knob(self, knob: int, value: int):
+        """Test hook (sdr_sgbm_debug_knob): DEBUG_SWEEP_SPIN = polls before a sweep wait gives up."""
+        check(lib().sdr_sgbm_debug_knob(self._h, int(knob), int(value)))
 
     def enable_timing(self, level=1):
         """0 off, 1 per-stage events, 2 per-stage + per-kernel-launch events."""

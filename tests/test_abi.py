@@ -21,7 +21,7 @@ def declared_functions():
 
 
 def test_library_loads():
-    assert _lib.lib().sdr_abi_version() == 3
+    assert _lib.lib().sdr_abi_version() == 4
 
 
 def test_every_declared_symbol_exported():
@@ -151,3 +151,19 @@ def test_chain_span_guard_host_only():
     assert L.sdr_sgbm_scratch_bytes(ctypes.byref(p), 1920, 1080, 1) > 0  # C5 fits
     assert L.sdr_sgbm_scratch_bytes(ctypes.byref(p), 8192, 1200, 1) == 0
     assert b"2 GiB" in L.sdr_last_error()
+
+
+def test_build_id_matches_sources():
+    """The library in the tree is the build of these sources (build.py source_hash), so the
+    prebuilt libsdr.so that travels to the GPU box cannot silently be an older build."""
+    from stereo_depth_ruler_amd.build import built_id, source_hash
+
+    assert _lib.lib().sdr_build_id().decode() == source_hash()
+    assert built_id() == source_hash()
+
+
+def test_sweep_status_host_only():
+    """sdr_sgbm_last_status / sdr_sgbm_debug_knob reject a null handle without touching a GPU."""
+    L = _lib.lib()
+    assert L.sdr_sgbm_last_status(None) == -1
+    assert L.sdr_sgbm_debug_knob(None, 1, 4) == -1

@@ -145,3 +145,56 @@ def test_check_ranks_single_process():
             check_ranks(-4)
     finally:
         dist.destroy_process_group()
+
+
+def _group_worker(rank, world, port, direct, q):
+    """world 3; ranks 0 and 1 gather over a subgroup {0, 1} while rank 2 stays out of it, or
+    (direct) the world is set up by torch.distributed.init_process_group itself, without the
+    wrapper's status group."""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if direct:
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
+    else:
+        from stereo_depth_ruler_amd.distributed import init_process_group
+        init_process_group("gloo", rank=rank, world_size=world, timeout=30)
+    local = torch.full((2, 4, 4), rank + 1, dtype=torch.int16)
+    out = None
+    if direct:
+        out = gather_frames(local, 2 * world, world, rank)
+    else:
+        g = dist.new_group([0, 1])
+        if rank < 2:
+            out = gather_frames(local, 4, 2, rank, group=g)
+    if rank == 0:
+        q.put(out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_gather_frames_subgroup_and_direct_init(direct):
+    """gather_frames' status exchange runs on the caller's group (a subgroup's ranks only) and works
+    on a world that init_process_group set up without the wrapper."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_group_worker, args=(r, world, port, direct, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    got = q.get(timeout=90)
+    for pr in procs:
+        pr.join(timeout=60)
+    alive = [pr for pr in procs if pr.is_alive()]
+    for pr in alive:
+        pr.kill()
+    assert not alive and all(pr.exitcode == 0 for pr in procs), [pr.exitcode for pr in procs]
+    nr = world if direct else 2
+    # frame i came from rank i mod nr, its (i // nr)-th local frame
+    assert got.shape[0] == 2 * nr
+    for i in range(2 * nr):
+        assert (got[i] == (i % nr) + 1).all(), i

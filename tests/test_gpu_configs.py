@@ -116,3 +116,42 @@ def test_c3_batch32_hh_d256(oracle):
         assert np.array_equal(out[i], single[0].cpu().numpy()), f"frame {i} differs from its single-frame run"
     m.close()
     m1.close()
+
+
+def test_c5_batch8_as_benched(oracle):
+    """C5 as bench.py --config c5 runs it: 8 distinct 3840x1080 side-by-side frames in
+    ONE CloudEmit batch, which takes the batched MODE_HH row sweeps (k_sweep) at 1920x1080, d=256.
+    Disparity, XYZ and the organised cloud of all 8 frames equal single-frame device runs (the
+    k_paths chains), frames 0 and 7 equal the oracle chain, and the handle reports no sweep
+    failure."""
+    W, H, F = 1920, 1080, 8
+    dev = torch.device("cuda", 0)
+    frames = [S.sbs_bgr_color_frame(H, W, 256, seed=700 + i) for i in range(F)]
+    sbs = torch.from_numpy(np.stack(frames)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    pipe = CloudEmit(W, H, C5_ARGS, F, S.REFERENCE_Q, leaf=0.005)
+    pipe.enqueue(sbs, stream, voxel=False)
+    torch.cuda.synchronize(dev)
+    pipe.matcher().check_status()
+    disp, xyz, pts = (pipe.disp.cpu().numpy(), pipe.xyz.cpu().numpy(), pipe.points.cpu().numpy())
+    one = CloudEmit(W, H, C5_ARGS, 1, S.REFERENCE_Q, leaf=0.005)
+    for i in range(F):
+        one.enqueue(sbs[i:i + 1], stream, voxel=False)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(disp[i], one.disp[0].cpu().numpy()), f"frame {i}: disparity differs from single"
+        assert np.array_equal(u32(xyz[i]), u32(one.xyz[0].cpu().numpy())), f"frame {i}: xyz"
+        assert np.array_equal(u32(pts[i]), u32(one.points[0].cpu().numpy())), f"frame {i}: cloud"
+    p = oracle.make_params(*C5_ARGS)
+
+    def ref_of(i):
+        left, right = frames[i][:, :W], frames[i][:, W:]
+        d = oracle.sgbm_compute(oracle.bgr2gray(left), oracle.bgr2gray(right), p)
+        return d, oracle.reproject(oracle.disp_to_float(d), S.REFERENCE_Q, True)
+
+    with ThreadPoolExecutor(2) as ex:
+        refs = list(ex.map(ref_of, (0, F - 1)))
+    for i, (d, rx) in zip((0, F - 1), refs):
+        assert np.array_equal(disp[i], d), f"frame {i}: {(disp[i] != d).sum()} px differ from the oracle"
+        assert np.array_equal(u32(xyz[i]), u32(rx)), f"frame {i}: xyz differs from the oracle"
+    pipe.close()
+    one.close()

@@ -113,6 +113,46 @@ def test_world2_bench_step_gather_loop():
     assert out["gather_check"] == {"step": 7, "ranks": 2, "ok": True}
 
 
+def test_bench_gpus2_self_launch():
+    """`python bench.py --gpus 2` with NO external launcher (the driver's N-GPU command minus
+    torch.distributed.run): bench.py starts both ranks itself (here over gloo, both on the box's one
+    GPU) and prints one line with n_gpus 2, both ranks' times and a good gather check."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "2",
+           "--dist-backend", "gloo", "--streams", "2", "--frames", "4", "--no-cpu-baseline", "--no-kernel-timing"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert out["gather_check"]["ok"] and out["gather_check"]["ranks"] == 2
+    assert out["ranks"]["world_size_seen"] == 2 and len(out["ranks"]["per_rank"]) == 2
+    assert {r["rank"] for r in out["ranks"]["per_rank"]} == {0, 1}
+    worst = max(r["ms_per_step"] for r in out["ranks"]["per_rank"])
+    assert abs(out["ms_per_step"] - worst) < 1e-3 + 1e-3 * worst
+
+
+def test_bench_gpus2_nccl_needs_two_gpus():
+    """Over RCCL every rank needs its own GPU: on a one-GPU box --gpus 2 fails loudly instead of
+    printing an N=1 number."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU: the RCCL path can run")
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-kernel-timing"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert res.returncode != 0
+    assert "need 2 GPUs" in res.stderr
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+
+
 def _failing_worker(rank, world, port, q):
     """Rank 1 asks the real engine for numDisparities = 20 (SDR_ERR_NUMDISP, OpenCV's assert)."""
     import sys

@@ -73,3 +73,60 @@ def test_hh_sweep_frames_per_slot_and_negative_min_disparity(oracle):
         ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
         assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
     m.close()
+
+
+def test_sweep_timeout_poisons_batch_and_reports(oracle):
+    """The failure contract of the row sweeps: with the neighbour waits cut to one
+    poll (debug knob), waits give up; the batch's frames then come back INVALID ((minD-1)*16 on
+    every pixel, never silently wrong values) and the handle's status reports SDR_ERR_DEVICE once.
+    The next batch with the default budget is bit-exact again and the status is clean."""
+    F, H, W, D = 16, 96, 1700, 48
+    args = (0, D, 5, 600, 2400, 1, 63, 10, 0, 2, sdr.MODE_HH)
+    Ls, Rs = _batch("textured", F, H, W, D, 40)
+    dev = torch.device("cuda", 0)
+    Ld, Rd = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    m = sdr.StereoSGBM.create(*args)
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 1)
+    bad = m.compute(Ld, Rd).cpu().numpy()
+    with pytest.raises(sdr.SDRError) as ei:
+        m.check_status()
+    assert ei.value.code == -6
+    assert (bad == -16).all(), "a timed-out sweep must leave no frame values behind"
+    m.check_status()  # reported once
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 0)
+    good = m.compute(Ld, Rd).cpu().numpy()
+    m.check_status()
+    p = oracle.make_params(*args)
+    for i in (0, F - 1):
+        assert np.array_equal(good[i], oracle.sgbm_compute(Ls[i], Rs[i], p)), i
+    m.close()
+
+
+def test_two_handles_two_streams_concurrent_sweeps(oracle):
+    """Two matchers on two streams each enqueue 8-frame MODE_HH batches back to back without a
+    synchronisation in between: their sweeps are chained per device (never two in flight), and
+    every frame equals its single-frame k_paths run."""
+    F, H, W, D = 8, 40, 600, 64
+    args = (0, D, 5, 600, 2400, 1, 63, 10, 20, 2, sdr.MODE_HH)
+    dev = torch.device("cuda", 0)
+    batches = [_batch("textured", F, H, W, D, 100 + 10 * k) for k in range(4)]
+    dev_in = [(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)) for L, R in batches]
+    ms = [sdr.StereoSGBM.create(*args) for _ in range(2)]
+    ss = [torch.cuda.Stream(dev) for _ in range(2)]
+    torch.cuda.synchronize(dev)
+    outs = []
+    for k, (Ld, Rd) in enumerate(dev_in):
+        with torch.cuda.stream(ss[k % 2]):
+            outs.append(ms[k % 2].compute(Ld, Rd))
+    torch.cuda.synchronize(dev)
+    for m in ms:
+        m.check_status()
+    one = sdr.StereoSGBM.create(*args)
+    for k, (L, R) in enumerate(batches):
+        got = outs[k].cpu().numpy()
+        for i in range(F):
+            assert np.array_equal(got[i], one.compute(L[i], R[i])), f"batch {k} frame {i}"
+    p = oracle.make_params(*args)
+    assert np.array_equal(outs[3][F - 1].cpu().numpy(), oracle.sgbm_compute(batches[3][0][F - 1], batches[3][1][F - 1], p))
+    for m in ms + [one]:
+        m.close()

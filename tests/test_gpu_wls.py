@@ -76,6 +76,21 @@ def test_fgs_stack_and_iterations(oracle, solver):
         assert np.array_equal(bits(got[i]), bits(ref))
 
 
+@pytest.mark.parametrize("shape", [(2, 1500), (3, 3000), (2, 3840), (3840, 2), (3, 4096), (4096, 3)])
+def test_pcr_long_lines(oracle, shape):
+    """k_fgs_pcr on lines past 1024 samples (2 and 4 equations per thread) and past the 3413 whose
+    double-buffered stages (48 B/sample) exceed a workgroup's 160 KiB of LDS, which then take the
+    single-buffered form (24 B/sample): rows (w long) and columns (h long), up to the 4096 limit.
+    A 4K frame's 3840-sample rows run here."""
+    rng = np.random.default_rng(shape[0] * 7 + shape[1])
+    g = rng.integers(0, 256, shape).astype(np.uint8)
+    x = (rng.random(shape) * 1000).astype(np.float32)
+    for lam, sigma in ((8000.0, 1.1), (50.0, 5.0)):
+        ref = oracle.fgs_filter(g, x, lam, sigma, solver=FGS_PCR)
+        got = fastGlobalSmootherFilter(g, x, lam, sigma, solver=FGS_PCR)
+        assert np.array_equal(bits(got), bits(ref)), (shape, lam)
+
+
 def test_pcr_line_limit():
     g = np.zeros((2, 4097), np.uint8)
     x = np.ones((2, 4097), np.float32)

@@ -1,4 +1,4 @@
 extern "C" const char* sdr_build_id(void) {
-    static const char id[] = "SDR_BUILD_ID=c6839c98eccecf25";
+    static const char id[] = "SDR_BUILD_ID=1cc5cdd882dbc63e";
     return id + 13;
 }

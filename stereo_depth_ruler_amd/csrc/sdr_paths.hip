@@ -181,15 +181,26 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
 
     // path-cost stores are non-temporal: measured on MI355X (C2, 2 frames in flight) +4 % fps
-    // over default-policy stores, the WTA's re-reads of the L buffers getting faster
+    // over default-policy stores, the WTA's re-reads of the L buffers getting faster.
+    // The store is unconditional: padding lanes (which alias the last word on loads) get a lane
+    // offset past the resource's num_records, so the hardware drops their writes.  A store under
+    // `if (active)` put a branch in every step, and the compiler's vmcnt accounting then had to
+    // assume the path where no store was issued: every step waited until only 15 memory ops
+    // were outstanding, i.e. for the C load of ~8 steps back instead of 16 -- the E/W chains of
+    // the padded D = 80 class path ran at the memory latency / 8 per step.
+    const uint32_t sofs_st = active ? lofs : 0x80000000u;
     auto step = [&](const int, auto jc) __attribute__((always_inline)) {
         constexpr int j = decltype(jc)::value;
         const Regs<K> c = cring[j];
         cring[(j + LA) % R] = load_buf<K>(rC, lofs, soff);
         soff += (uint32_t)rowb;
         const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
-        if (active) store_buf_nt<K>(rO, lofs, soffl, L);  // padding lanes alias the last word
+        store_buf_nt<K>(rO, sofs_st, soffl, L);
         soffl += (uint32_t)rowl;
+        // one scheduling region per step (as the branch used to make it): scheduled across the
+        // whole unrolled ring, the steps' loads and stores were reordered and the ring registers
+        // copied, with vmcnt(0) waits inside the loop
+        __builtin_amdgcn_sched_barrier(0);
     };
     int k0 = 0;
     for (; k0 + R <= ch.len; k0 += R) {

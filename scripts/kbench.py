@@ -25,6 +25,7 @@ CONFIGS = {  # W, H, D, mode, frames
     "c3": (1280, 720, 256, 1, 8),
     "c0": (640, 360, 80, 2, 1),
     "c5": (1920, 1080, 256, 1, 1),
+    "c4": (640, 360, 80, 2, 2),  # the class path's two matchers as two frames (1440 E/W chains)
 }
 KINDS = ["prefilter", "k_cost", "k_paths", "k_south_wta", "median", "speckle", "reproject", "k_lr_check"]
 

@@ -45,8 +45,12 @@ struct CostCfg {
     // row prefetch depth and the row loop's unroll: U covers the ring slot (% NR), the LDS
     // double buffer (% 2) and the prefetch register slot (% PD) statically
     // (two rows: deeper prefetch costs registers, i.e. resident blocks, and measured slower)
-    static constexpr int PD = 2;
-    static constexpr int U = 2 * NR;
+#ifndef SDR_COST_PD
+#define SDR_COST_PD 2
+#endif
+    static constexpr int PD = SDR_COST_PD;
+    static constexpr int gcd(int a, int b) { return b ? gcd(b, a % b) : a; }
+    static constexpr int U = 2 * NR / gcd(2 * NR, PD) * PD;  // lcm(2 NR, PD)
     // LDS bytes: two staging buffers (R: 3 pair planes x 2 parity halves, L: 4 words a column,
     // each per operand set) + two column-sum buffers
     static size_t lds_bytes(int D) {

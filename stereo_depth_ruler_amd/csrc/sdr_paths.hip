@@ -211,9 +211,162 @@ __global__ __launch_bounds__(256) void k_paths(Geometry g, PathLaunch pl) {
     unroll_rows_tail(step, k0, last, std::make_integer_sequence<int, R - 1>{});
 }
 
+// k_paths with TWO chains per wave (lanes 0-31: chain 2w, lanes 32-63: chain 2w+1 of the same
+// direction), four disparities (two packed pairs) per lane, for the latency-bound launches: D <=
+// 128 and more chains than SIMDs but few enough that each chain waits on its own serial steps.
+// The class path's paired 3WAY matchers at 640x360 have 1440 E/W chains of 560 steps: one per
+// wave, 416 SIMDs held two and every such chain ran ~1.6x slower (C4 k_paths 85 us, against 54
+// for the 720 chains of one matcher); two per wave, all 720 waves have a SIMD to themselves, and a
+// step costs about the same instructions for two chains as the one-chain step for one.
+//   - the d +- 1 neighbours cross lanes by the same DPP wave shifts, with lane 32 (31) given the
+//     chain's boundary value instead of the other chain's lane 31 (32);
+//   - the per-chain minimum: DPP row minima, row_bcast:15 into rows 1 and 3 (lanes 31 and 63 then
+//     hold the two halves' minima), two readlanes, and the half's delta selected per lane;
+//   - one buffer resource per wave based at chain A; chain B's lanes carry the (non-negative)
+//     distance to chain B in their offset.  Only directions whose chains all have one length (E, W,
+//     N, S) take this kernel, so the two chains step together.
+// One step of two chains (lanes 0-31: chain A, 32-63: chain B; two packed pairs per lane):
+// path_step with the chains' boundary lanes fed their own fill and a per-half minimum.
+template <bool PAD>
+__device__ __forceinline__ Regs<2> path_step_tc(Regs<2> c, Regs<2>& Lp, uint32_t& delta2, uint32_t P1x2,
+                                                uint32_t P2x2, bool active, uint32_t& upr, uint32_t& dnr,
+                                                int lane) {
+    constexpr int K = 2;
+    if constexpr (PAD) {
+#pragma unroll
+        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
+    }
+    upr = lane_from_prev(Lp.r[K - 1], upr);
+    dnr = lane_from_next(Lp.r[0], dnr);
+    const uint32_t up = lane == 32 ? kMaxPair : upr;  // chain B's first lane: its own boundary
+    const uint32_t dn = lane == 31 ? kMaxPair : dnr;
+    Regs<K> L;
+    uint32_t m = kMaxPair;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
+        const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
+        uint32_t t = pk_add_sat(pk_min(dm1, dp1), P1x2);
+        t = pk_min(pk_min(t, Lp.r[i]), delta2);
+        uint32_t l = pk_sub(pk_add(c.r[i], t), delta2);
+        if constexpr (PAD) l = active ? l : kMaxPair;
+        L.r[i] = l;
+        m = pk_min(m, l);
+    }
+    // the two chains' minima: 16-lane rows, then rows 0+1 and 2+3 (row_bcast:15 into rows 1, 3)
+    uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu), (unsigned short)(m >> 16));
+    m16 = row16_min_u32(m16);
+    m16 = min(m16, (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m16, 0x142, 0xa, 0xf, false));
+    const uint32_t dA = (uint32_t)__builtin_amdgcn_readlane((int)m16, 31) * 0x00010001u + P2x2;
+    const uint32_t dB = (uint32_t)__builtin_amdgcn_readlane((int)m16, 63) * 0x00010001u + P2x2;
+    delta2 = lane >= 32 ? dB : dA;
+    Lp = L;
+    return L;
+}
+
+template <bool PAD>
+__global__ __launch_bounds__(256) void k_paths_tc(Geometry g, PathLaunch pl) {
+    constexpr int DPL = 4, K = 2;
+    constexpr int LA = paths_la<DPL>();
+    constexpr int R = 2 * LA;
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5, hl = lane & 31;
+    const int wg = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int f = blockIdx.y;
+    int di = 0, w0 = 0;
+    for (; di < pl.ndirs; di++) {
+        const int nw = (pl.d[di].nchains + 1) / 2;
+        if (wg < w0 + nw) break;
+        w0 += nw;
+    }
+    if (di >= pl.ndirs) return;
+    const PathDir pd = pl.d[di];
+    const int ca = 2 * (wg - w0);
+    const bool hasB = ca + 1 < pd.nchains;
+    const Chain ch = make_chain(g, pd, ca);
+    const Chain chB = make_chain(g, pd, hasB ? ca + 1 : ca);
+    if (ch.len <= 0) return;
+
+    const int D = g.D, W1 = g.W1;
+    const bool active = (half == 0 || hasB) && (!PAD || hl * DPL < D);
+    const uint32_t lofs = (uint32_t)((PAD ? min(hl, D / DPL - 1) : hl) * DPL * 2);
+    const ptrdiff_t pixB = (ptrdiff_t)(chB.y0 - ch.y0) * W1 + (chB.x0 - ch.x0);  // >= 0
+    const ptrdiff_t rowb = (ptrdiff_t)(ch.dy * W1 + ch.dx) * D * 2;
+    const ptrdiff_t rowl = (ptrdiff_t)(ch.dy * W1 + ch.dx) * pl.l_pix * 2;
+    const uint32_t vld = lofs + (half ? (uint32_t)(pixB * D * 2) : 0u);
+    const uint32_t vst = active ? lofs + (half ? (uint32_t)(pixB * pl.l_pix * 2) : 0u) : 0x80000000u;
+    const char* cp = (const char*)(pl.C + (size_t)f * pl.cs_fstride + ((size_t)ch.y0 * W1 + ch.x0) * D);
+    char* op = (char*)(pd.out + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
+    const int last = ch.len - 1;
+    const int low = rowb >= 0 ? 0 : last + LA;
+    const Rsrc rC = rsrc_at(cp + (ptrdiff_t)low * rowb);
+    uint32_t soff = (uint32_t)((ptrdiff_t)(0 - low) * rowb);
+    Rsrc rO;
+    uint32_t soffl = 0;
+    auto rebase = [&](int k0) __attribute__((always_inline)) {
+        const int lo = rowl >= 0 ? k0 : k0 + R - 1;
+        rO = rsrc_at(op + (ptrdiff_t)lo * rowl);
+        soffl = (uint32_t)((ptrdiff_t)(k0 - lo) * rowl);
+    };
+    Regs<K> cring[R];
+#pragma unroll
+    for (int j = 0; j < LA; j++) {
+        cring[j] = load_buf<K>(rC, vld, soff);
+        soff += (uint32_t)rowb;
+    }
+    Regs<K> Lp;
+#pragma unroll
+    for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
+    const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
+    uint32_t delta2 = P2x2;
+    uint32_t upr = kMaxPair, dnr = kMaxPair;
+    auto step = [&](const int, auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const Regs<K> c = cring[j];
+        cring[(j + LA) % R] = load_buf<K>(rC, vld, soff);
+        soff += (uint32_t)rowb;
+        const Regs<K> L = path_step_tc<PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr, lane);
+        store_buf_nt<K>(rO, vst, soffl, L);
+        soffl += (uint32_t)rowl;
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int k0 = 0;
+    for (; k0 + R <= ch.len; k0 += R) {
+        rebase(k0);
+        unroll_rows(step, k0, std::make_integer_sequence<int, R>{});
+    }
+    rebase(k0);
+    unroll_rows_tail(step, k0, last, std::make_integer_sequence<int, R - 1>{});
+}
+
+// the two-chain kernel for this launch?  D <= 128, no redirected 3WAY rows, every direction with
+// chains of one length, and more chains than the chip's SIMDs (with fewer, one chain per wave
+// already has a SIMD each and the one-chain step is the cheaper one)
+static bool paths_two_chain(const Geometry& g, const PathLaunch& pl, int F) {
+    if (g.D > 128 || pl.nredir > 0) return false;
+    for (int i = 0; i < pl.ndirs; i++)
+        if (pl.d[i].dir != DIR_E && pl.d[i].dir != DIR_W && pl.d[i].dir != DIR_N) return false;
+    static thread_local int simds = 0;
+    if (!simds) {
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        simds = 4 * (cus > 0 ? cus : 256);
+    }
+    return (long)pl.prefix[pl.ndirs] * F > simds;
+}
+
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st) {
     const int total = pl.prefix[pl.ndirs];
     if (total <= 0) return;
+    if (paths_two_chain(g, pl, F)) {
+        int waves = 0;
+        for (int i = 0; i < pl.ndirs; i++) waves += (pl.d[i].nchains + 1) / 2;
+        const dim3 grid2((waves + 3) / 4, F);
+        if (g.D < 128) hipLaunchKernelGGL((k_paths_tc<true>), grid2, dim3(256), 0, st, g, pl);
+        else hipLaunchKernelGGL((k_paths_tc<false>), grid2, dim3(256), 0, st, g, pl);
+        return;
+    }
     dim3 grid((total + 3) / 4, F);
     if (g.D <= 128) {
         if (g.D < 128) hipLaunchKernelGGL((k_paths<2, true>), grid, dim3(256), 0, st, g, pl);
@@ -581,22 +734,36 @@ void launch_sweep(const Geometry& g, const SweepArgs& a, int F, hipStream_t st) 
 // ------------------------------------------------------------------------------------------
 // 1 producer + 3 consumer waves (256 threads): the 1152 column chains of a 1280x720 d=128 frame
 // are resident in one pass.  2 and 4 consumer waves measured the same within noise.
-constexpr int kSouthConsumers = 3;
+#ifndef SDR_SOUTH_CONS
+#define SDR_SOUTH_CONS 3
+#endif
+#ifndef SDR_SOUTH_LAB
+#define SDR_SOUTH_LAB 2
+#endif
+constexpr int kSouthConsumers = SDR_SOUTH_CONS;
 constexpr int kSouthRPW = 4;                           // rows per consumer wave and block (4 per pass;
                                                        // 8 rows x 2 consumers measured the same)
 constexpr int kSouthRB = kSouthRPW * kSouthConsumers;  // rows per block
-constexpr int kSouthLAB = 2;                   // producer lookahead in blocks (C0 -28 %, C2 -3 % vs 1)
+constexpr int kSouthLAB = SDR_SOUTH_LAB;       // producer lookahead in blocks (C0 -28 %, C2 -3 % vs 1)
 constexpr int kSouthSPad = 4;                  // dword padding of the consumers' staged S rows
 constexpr int kStageBlocks = 32;               // blocks per output staging window
 constexpr int kStageRows = kStageBlocks * kSouthRB;
 constexpr uint32_t kNoWrite = 0xfffffffeu;     // staged row outside this chain's output rows
 constexpr uint32_t kRejected = 0xffffffffu;    // no disp2 candidate
 
-template <int DPL, bool PAD, int NP>
+// TC (two columns per workgroup, D <= 128, DPL = 2): the producer wave runs the chains of two
+// adjacent columns of one direction entry, lanes 0-31 and 32-63 with four disparities each (the
+// k_paths_tc step), and the consumers take both columns' pixels of a block (two passes).  The
+// class path's 3WAY stripes at 640x360 are 4480 short chains of ~100 rows, each a workgroup whose
+// producer's serial steps bound the pass; two per workgroup halves the workgroups to run.
+template <int DPL, bool PAD, int NP, bool TC = false>
 __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geometry g0, PathLaunch pl,
                                                                            SouthWtaArgs a) {
+    static_assert(!TC || DPL == 2, "two columns per workgroup: the D <= 128 layout");
     const Geometry g = frame_geom(g0, blockIdx.y);
     constexpr int K = DPL / 2;
+    constexpr int NCOL = TC ? 2 : 1;   // columns per workgroup
+    constexpr int PK = TC ? 2 : K;     // producer words per lane
     constexpr int RB = kSouthRB;
     constexpr int LAB = kSouthLAB;
     constexpr int LA = LAB * RB;  // producer lookahead in rows
@@ -611,24 +778,39 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     constexpr int LSTR = DMAX / 2 + 4;  // dwords per staged row (padded: rows of a wave's 4 pixels)
     // consumer prefetch distance in blocks (= ring slots) of the other directions' L
     // (two blocks while the ring fits 64 VGPRs; 1 block -- a ring of 56 VGPRs -- for 8 paths at D > 128)
-    constexpr int PD = NP * WK * kSouthRPW <= 128 ? 2 : 1;
+    constexpr int PD = NP * WK * kSouthRPW * NCOL <= 128 ? 2 : 1;
     static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
-    __shared__ uint32_t sL[2][RB][LSTR];
+    __shared__ uint32_t sL[2][RB][NCOL][LSTR];
     // each consumer row's S staged for the subpixel neighbours and the uniqueness minimum (one
     // 16-B write per lane, three masking u16 writes, one read back); rows padded by 4 dwords so
     // the four lane groups' 16-B writes start on different banks
     __shared__ uint32_t sS[kSouthConsumers][4][DMAX / 2 + kSouthSPad];
     // per-row outputs, two windows of kStageRows rows
-    __shared__ int16_t sRaw[2][kStageRows];
-    __shared__ uint32_t sKey[2][kStageRows];
+    __shared__ int16_t sRaw[2][NCOL][kStageRows];
+    __shared__ uint32_t sKey[2][NCOL][kStageRows];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // role (0 = producer)
     const int cg = blockIdx.x;
     const int f = blockIdx.y;
-    int di = 0;
-    while (cg >= pl.prefix[di + 1]) di++;
+    int di = 0, c0i = 0;
+    bool hasB = false;
+    if constexpr (TC) {
+        // workgroups per direction entry: ceil(chains / 2)
+        int w0 = 0;
+        for (; di < pl.ndirs; di++) {
+            const int nw = (pl.d[di].nchains + 1) / 2;
+            if (cg < w0 + nw) break;
+            w0 += nw;
+        }
+        if (di >= pl.ndirs) return;
+        c0i = 2 * (cg - w0);
+        hasB = c0i + 1 < pl.d[di].nchains;
+    } else {
+        while (cg >= pl.prefix[di + 1]) di++;
+        c0i = cg - pl.prefix[di];
+    }
     const PathDir pd = pl.d[di];
-    const Chain ch = make_chain(g, pd, cg - pl.prefix[di]);
+    const Chain ch = make_chain(g, pd, c0i);  // TC: the second column is ch.x0 + 1, same rows
     if (ch.len <= 0) return;  // whole workgroup
     const int D = g.D, W1 = g.W1;
     const size_t fofs = (size_t)f * pl.cs_fstride;
@@ -638,8 +820,11 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     if (wv == 0) {
         // ---------------- producer: the recurrence, L rows to LDS ----------------
         __builtin_amdgcn_s_setprio(2);
-        const bool active = !PAD || lane * DPL < D;
-        const uint32_t lofs = (uint32_t)((PAD ? min(lane, D / DPL - 1) : lane) * DPL * 2);
+        // TC: half h of the wave runs column x0 + h (its lanes' offsets one pixel further)
+        const int half = TC ? lane >> 5 : 0, hl = TC ? lane & 31 : lane;
+        constexpr int PDPL = 2 * PK;  // producer disparities per lane
+        const bool active = (!TC || half == 0 || hasB) && (!PAD || hl * PDPL < D);
+        const uint32_t lofs = (uint32_t)((PAD ? min(hl, D / PDPL - 1) : hl) * PDPL * 2) + (uint32_t)(half * D * 2);
         const ptrdiff_t rowb = (ptrdiff_t)W1 * D * 2;
         // 3WAY stripes: a chain starting at aux_row0 reads its first aux_rows (< LA) cost rows
         // from the stripe-local (row-major) buffer; every later row comes from C
@@ -653,26 +838,28 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         // the class path's 3WAY stripes are ~100 rows, and a lookahead of LA rows past each
         // stripe's end was a quarter of the pass's HBM reads there
         auto crow = [&](int k) { return c0 + (ptrdiff_t)min(k, last) * rowb; };
-        Regs<K> cring[R];
+        Regs<PK> cring[R];
 #pragma unroll
         for (int j = 0; j < LA; j++)
-            cring[j] = load_buf<K>(rsrc_at(j < naux ? abase + (ptrdiff_t)j * rowb : crow(j)), lofs);
-        Regs<K> Lp;
+            cring[j] = load_buf<PK>(rsrc_at(j < naux ? abase + (ptrdiff_t)j * rowb : crow(j)), lofs);
+        Regs<PK> Lp;
 #pragma unroll
-        for (int i = 0; i < K; i++) Lp.r[i] = active ? 0u : kMaxPair;
+        for (int i = 0; i < PK; i++) Lp.r[i] = active ? 0u : kMaxPair;
         const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
         uint32_t delta2 = P2x2;
         uint32_t upr = kMaxPair, dnr = kMaxPair;  // see path_step
         // block bb (= slot ic of the ring): RB recurrence steps into LDS slot bb & 1, then hand over
         auto block = [&](const int bb, auto ic) __attribute__((always_inline)) {
-            uint32_t* dst = &sL[bb & 1][0][lane * K];
+            uint32_t* dst = &sL[bb & 1][0][half][hl * PK];
             auto st = [&](const int, auto jc) __attribute__((always_inline)) {
                 constexpr int j = decltype(jc)::value + decltype(ic)::value * RB;  // ring slot = k % R
-                const Regs<K> c = cring[j];
-                cring[(j + LA) % R] = load_buf<K, kLoadNT>(rsrc_at(crow(bb * RB + (j % RB) + LA)), lofs);
-                const Regs<K> L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
+                const Regs<PK> c = cring[j];
+                cring[(j + LA) % R] = load_buf<PK, kLoadNT>(rsrc_at(crow(bb * RB + (j % RB) + LA)), lofs);
+                Regs<PK> L;
+                if constexpr (TC) L = path_step_tc<PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr, lane);
+                else L = path_step<K, PAD>(c, Lp, delta2, P1x2, P2x2, active, upr, dnr);
 #pragma unroll
-                for (int i = 0; i < K; i++) dst[(j % RB) * LSTR + i] = L.r[i];
+                for (int i = 0; i < PK; i++) dst[(j % RB) * NCOL * LSTR + i] = L.r[i];
             };
             unroll_rows(st, bb * RB, std::make_integer_sequence<int, RB>{});
             __syncthreads();
@@ -685,7 +872,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     }
 
     // ---------------- consumers: the other directions + WTA, RPW rows per wave ----------------
-    constexpr int NPASS = kSouthRPW / 4;  // passes of 4 rows (one per 16-lane group)
+    // passes of 4 pixels (one per 16-lane group): the wave's RPW rows of each column
+    constexpr int RPASS = kSouthRPW / 4;
+    constexpr int NPASS = NCOL * RPASS;
     const int gl = lane & 15, grp = lane >> 4;
     // D > 256: 32 disparities per lane, so the last active lane may hold fewer than 32 (D is a
     // multiple of 16): it reads its own offset and masks the pairs past D (see ssum)
@@ -698,8 +887,9 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     uint32_t lofs[NPASS];
 #pragma unroll
     for (int ps = 0; ps < NPASS; ps++) {
-        rr[ps] = (wv - 1) * kSouthRPW + ps * 4 + grp;
-        lofs[ps] = (uint32_t)(((size_t)rr[ps] * W1 * pl.l_pix + wd0) * 2);
+        const int col = ps / RPASS;  // TC: passes of the second column are one pixel further on
+        rr[ps] = (wv - 1) * kSouthRPW + (ps % RPASS) * 4 + grp;
+        lofs[ps] = (uint32_t)((((size_t)rr[ps] * W1 + col) * pl.l_pix + wd0) * 2);
     }
     const char* lbase = (const char*)(a.L + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
     // blocks past the chain's last one re-read that block (L2 hits), not the buffers' slack
@@ -723,23 +913,28 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     auto flush = [&](int w) __attribute__((always_inline)) {
         const int r0 = w * kStageRows;
         const int n = min(kStageRows, ch.len - r0);
-        for (int i = (wv - 1) * 64 + lane; i < n; i += 64 * kSouthConsumers) {
-            const uint32_t key = sKey[w & 1][i];
-            if (key == kNoWrite) continue;
-            const size_t y = (size_t)(ch.y0 + r0 + i);
-            raw[y * g.W] = sRaw[w & 1][i];
-            if (d2 && key < kNoWrite) {
-                // A.8's disp2 candidate of this pixel (no return value: a fire-and-forget atomic)
-                const int x2 = x2base - (int)(key & 0xffff);
-                if (x2 >= 0 && x2 < g.W) atomicMin(&d2[y * g.W + x2], (key & 0xffff0000u) | (uint32_t)(0xffff - x));
+#pragma unroll
+        for (int col = 0; col < NCOL; col++) {
+            if (col > 0 && !hasB) break;  // uniform
+            for (int i = (wv - 1) * 64 + lane; i < n; i += 64 * kSouthConsumers) {
+                const uint32_t key = sKey[w & 1][col][i];
+                if (key == kNoWrite) continue;
+                const size_t y = (size_t)(ch.y0 + r0 + i);
+                raw[y * g.W + col] = sRaw[w & 1][col][i];
+                if (d2 && key < kNoWrite) {
+                    // A.8's disp2 candidate of this pixel (no return value: a fire-and-forget atomic)
+                    const int x2 = x2base + col - (int)(key & 0xffff);
+                    if (x2 >= 0 && x2 < g.W)
+                        atomicMin(&d2[y * g.W + x2], (key & 0xffff0000u) | (uint32_t)(0xffff - (x + col)));
+                }
             }
         }
     };
 
     // one 4-row pass of block b: S of row k = b*RB + r, the WTA, its outputs staged in LDS
     // S = sat(sum of the P path costs) of row r of block b, the fused direction's L from LDS
-    auto ssum = [&](const int b, const int r, const Regs<WK> (&o)[NP]) __attribute__((always_inline)) {
-        const uint32_t* ls = &sL[b & 1][r][wd0 / 2];
+    auto ssum = [&](const int b, const int r, const int col, const Regs<WK> (&o)[NP]) __attribute__((always_inline)) {
+        const uint32_t* ls = &sL[b & 1][r][col][wd0 / 2];
         Regs<WK> St;
 #pragma unroll
         for (int i = 0; i < WK; i++) {
@@ -754,7 +949,7 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         }
         return St;
     };
-    auto rows = [&](const int b, const int r, const Regs<WK>& St) __attribute__((always_inline)) {
+    auto rows = [&](const int b, const int r, const int col, const Regs<WK>& St) __attribute__((always_inline)) {
         const int k = b * RB + r;
         const bool rowok = k >= kw && k <= last;
         // first minimum: packed (S + 32768) << 16 | d keys, min over the 16-lane row
@@ -809,8 +1004,8 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
                     okey = ((uint32_t)minS << 16) | (uint32_t)best;
                 }
             }
-            sRaw[(k / kStageRows) & 1][k % kStageRows] = (int16_t)out;
-            sKey[(k / kStageRows) & 1][k % kStageRows] = okey;
+            sRaw[(k / kStageRows) & 1][col][k % kStageRows] = (int16_t)out;
+            sKey[(k / kStageRows) & 1][col][k % kStageRows] = okey;
         }
     };
 
@@ -830,10 +1025,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
         constexpr int s = decltype(sc)::value;
 #pragma unroll
         for (int ps = 0; ps < NPASS; ps++) {
-            const Regs<WK> St = ssum(b, rr[ps], oring[s][ps]);
+            const Regs<WK> St = ssum(b, rr[ps], ps / RPASS, oring[s][ps]);
 #pragma unroll
             for (int q = 0; q < NP; q++) oring[s][ps][q] = oload(q, b + PD, ps);
-            rows(b, rr[ps], St);
+            if (ps < RPASS || hasB) rows(b, rr[ps], ps / RPASS, St);  // TC: a second column exists
         }
         __syncthreads();
         // the window this block completes (or the chain's last, partial one) goes out now that
@@ -863,6 +1058,27 @@ static void launch_south_np(const Geometry& g, const PathLaunch& pl, const South
                             hipStream_t st) {
     dim3 grid(pl.prefix[pl.ndirs], F);
     dim3 block(64 * (1 + kSouthConsumers));
+    if constexpr (DPL == 2) {
+        // two columns per workgroup when the chains far outnumber what the chip holds at once
+        // (short, latency-bound chains: the class path's 3WAY stripes), up to 5 paths
+        static thread_local int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (cus <= 0) cus = 256;
+        }
+        if (a.npaths <= 5 && (long)pl.prefix[pl.ndirs] * F > 8L * cus) {
+            int wgs = 0;
+            for (int i = 0; i < pl.ndirs; i++) wgs += (pl.d[i].nchains + 1) / 2;
+            const dim3 grid2(wgs, F);
+            switch (a.npaths) {
+            case 3: hipLaunchKernelGGL((k_south_wta<2, PAD, 2, true>), grid2, block, 0, st, g, pl, a); return;
+            case 4: hipLaunchKernelGGL((k_south_wta<2, PAD, 3, true>), grid2, block, 0, st, g, pl, a); return;
+            default: hipLaunchKernelGGL((k_south_wta<2, PAD, 4, true>), grid2, block, 0, st, g, pl, a); return;
+            }
+        }
+    }
     switch (a.npaths) {
     case 3: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 2>), grid, block, 0, st, g, pl, a); break;
     case 4: hipLaunchKernelGGL((k_south_wta<DPL, PAD, 3>), grid, block, 0, st, g, pl, a); break;

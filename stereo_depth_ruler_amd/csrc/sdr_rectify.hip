@@ -73,14 +73,26 @@ __device__ __forceinline__ void remap_px(const uint8_t* __restrict__ src, int sw
     const int w10 = (32 - ax) * ay * 32, w11 = ax * ay * 32;
     const bool x0 = sx >= 0 && sx < sw, x1 = sx + 1 >= 0 && sx + 1 < sw;
     const bool y0 = sy >= 0 && sy < sh, y1 = sy + 1 >= 0 && sy + 1 < sh;
-    const uint8_t* r0 = src + (size_t)sy * sstride + (ptrdiff_t)sx * CN;
-    const uint8_t* r1 = r0 + sstride;
+    // every tap is loaded from a clamped, valid address and masked afterwards (BORDER_CONSTANT 0):
+    // loads under a condition made the compiler branch around each one and wait for it there
+    const int cx0 = min(max(sx, 0), sw - 1), cx1 = min(max(sx + 1, 0), sw - 1);
+    const int cy0 = min(max(sy, 0), sh - 1), cy1 = min(max(sy + 1, 0), sh - 1);
+    const uint8_t* r0 = src + (size_t)cy0 * sstride;
+    const uint8_t* r1 = src + (size_t)cy1 * sstride;
+    int t[4][CN];
 #pragma unroll
     for (int c = 0; c < CN; c++) {
-        const int v00 = (x0 && y0) ? r0[c] : 0;
-        const int v01 = (x1 && y0) ? r0[CN + c] : 0;
-        const int v10 = (x0 && y1) ? r1[c] : 0;
-        const int v11 = (x1 && y1) ? r1[CN + c] : 0;
+        t[0][c] = r0[cx0 * CN + c];
+        t[1][c] = r0[cx1 * CN + c];
+        t[2][c] = r1[cx0 * CN + c];
+        t[3][c] = r1[cx1 * CN + c];
+    }
+#pragma unroll
+    for (int c = 0; c < CN; c++) {
+        const int v00 = (x0 && y0) ? t[0][c] : 0;
+        const int v01 = (x1 && y0) ? t[1][c] : 0;
+        const int v10 = (x0 && y1) ? t[2][c] : 0;
+        const int v11 = (x1 && y1) ? t[3][c] : 0;
         const int acc = v00 * w00 + v01 * w01 + v10 * w10 + v11 * w11;
         out[c] = min(max((acc + (1 << 14)) >> 15, 0), 255);
     }
@@ -132,20 +144,29 @@ __global__ __launch_bounds__(256) void k_sbs_ingest(SbsArgs a) {
     const uint16_t* m2 = a.map2[eye];
     uint8_t* bgr = a.bgr[eye] ? a.bgr[eye] + (size_t)f * W * H * 3 : nullptr;
     int gsum = 0;
+    // the block's four map entries first (clamped to the image: an odd size's missing pixels are
+    // computed on a duplicate and dropped), then every gather, all unconditional
+    uint32_t e1[4], e2[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const size_t o = (size_t)min(2 * y2 + (q >> 1), H - 1) * W + min(2 * x2 + (q & 1), W - 1);
+        e1[q] = m1[o];
+        e2[q] = m2[o];
+    }
+    int v[4][3];
+#pragma unroll
+    for (int q = 0; q < 4; q++) remap_px<3>(src, W, H, a.sstride, e1[q], e2[q], v[q]);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int x = 2 * x2 + (q & 1), y = 2 * y2 + (q >> 1);
         if (x >= W || y >= H) continue;
-        const size_t o = (size_t)y * W + x;
-        int v[3];
-        remap_px<3>(src, W, H, a.sstride, m1[o], m2[o], v);
         if (bgr) {
-            uint8_t* d = bgr + o * 3;
-            d[0] = (uint8_t)v[0];
-            d[1] = (uint8_t)v[1];
-            d[2] = (uint8_t)v[2];
+            uint8_t* d = bgr + ((size_t)y * W + x) * 3;
+            d[0] = (uint8_t)v[q][0];
+            d[1] = (uint8_t)v[q][1];
+            d[2] = (uint8_t)v[q][2];
         }
-        gsum += bgr2gray(v[0], v[1], v[2]);
+        gsum += bgr2gray(v[q][0], v[q][1], v[q][2]);
     }
     if (a.small[eye] && x2 < w2 && y2 < h2)
         a.small[eye][(size_t)f * w2 * h2 + (size_t)y2 * w2 + x2] = (uint8_t)((gsum + 2) >> 2);

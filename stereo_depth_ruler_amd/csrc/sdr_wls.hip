@@ -82,6 +82,36 @@ struct WlsGeom {
     int fill;                // 16 * (min_disp - 1)
 };
 
+// The filter's outputs (the class path's epilogue: fout = out / 16, xyz = reprojectImageTo3D(fout,
+// Q), both nullable), written by whichever kernel holds a pixel's final value: k_wls_final, or,
+// with SDR_FGS_PCR, k_wls_prep (pixels outside the ROI) and the last FGS column pass (the ROI).
+struct WlsOut {
+    int16_t* out;
+    float* fout;
+    float* xyz;
+    Q16 Q;
+};
+
+// saturate_cast<short>(FGS(conf*d) / FGS(conf)) (cv::divide of floats: 0 for a zero divisor;
+// cvRound = cvtss2si: NaN / |v| >= 2^31 give INT_MIN, which saturates to -32768)
+__device__ __forceinline__ int16_t wls_value(float a, float c) {
+    const float v = c != 0.0f ? a / c : 0.0f;
+    float q = rintf(v);
+    q = fminf(fmaxf(q, -32768.0f), 32767.0f);
+    return fabsf(v) < 2147483648.0f ? (int16_t)(int)q : (int16_t)-32768;
+}
+
+// pixel (x, y) of frame f: the int16 value and the epilogue
+__device__ __forceinline__ void wls_emit(const WlsOut& o, const WlsGeom& g, int f, int x, int y, int16_t r) {
+    const size_t p = (size_t)f * g.W * g.H + (size_t)y * g.W + x;
+    o.out[p] = r;
+    if (o.fout) {
+        const float df = (float)r * 0.0625f;
+        o.fout[p] = df;
+        if (o.xyz) reproject_px(o.Q, x, y, (double)df, 0.0, 0, o.xyz + 3 * p);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_wls_disc(const int16_t* __restrict__ dr, WlsGeom g,
                                                   float* __restrict__ rdisc) {
     const int j = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -282,10 +312,12 @@ constexpr int kPcrMaxN = 4096;  // samples per block (G * n): 4 equations per th
 // DB: the stage buffers double-buffered (48 B of LDS per sample, one barrier per stage), or single
 // (24 B per sample, two barriers per stage) for blocks whose 48 B per sample exceed the
 // workgroup's LDS (160 KiB on gfx950: past 3413 samples)
-template <int EPT, bool TWO, bool DB = true>
+// FIN (the last column pass, both right-hand sides): instead of storing the solved A, B back, the
+// block writes the filter's outputs for its ROI pixels (wls_value / wls_emit; gw = the geometry)
+template <int EPT, bool TWO, bool DB = true, bool FIN = false>
 __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const float* __restrict__ Cw,
                                                   int w, int h, size_t fstride, int rows, int G,
-                                                  float lam) {
+                                                  float lam, WlsGeom gw = {}, WlsOut wo = {}) {
     extern __shared__ float4 pcr_smem[];
     constexpr int NB = DB ? 2 : 1;
     const int T = blockDim.x;
@@ -413,8 +445,13 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
         const size_t off = addr(idx, g, k);
         if (l0 + g >= nlines) continue;
         const float4 x = Xo[g * n + k];
-        U0[fo + off] = x.z;
-        if constexpr (TWO) U1[fo + off] = x.w;
+        if constexpr (FIN) {
+            // columns pass: line l0 + g is ROI column j, sample k its ROI row i
+            wls_emit(wo, gw, lb / gx, gw.rx + l0 + g, gw.ry + k, wls_value(x.z, x.w));
+        } else {
+            U0[fo + off] = x.z;
+            if constexpr (TWO) U1[fo + off] = x.w;
+        }
     }
 }
 
@@ -482,17 +519,23 @@ __global__ __launch_bounds__(256) void k_transpose2(const float* __restrict__ s0
 //      sequential sweep, Cv row-major)
 // Rows outside the ROI only get the confidence map's 255.  Dynamic LDS: 32 B per ROI column
 // (int64 + int32 column sums and a float discontinuity value, per map).
+template <int RMAX>
 __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl, const int16_t* __restrict__ dr,
                                                   WlsGeom g, const uint8_t* __restrict__ guide,
                                                   size_t gstride, size_t gfstride,
                                                   const float* __restrict__ lut, int ch_rowmajor,
                                                   float* __restrict__ conf_full, float* __restrict__ A,
                                                   float* __restrict__ B, float* __restrict__ ChW,
-                                                  float* __restrict__ Cv) {
+                                                  float* __restrict__ Cv, int border, WlsOut wo) {
     extern __shared__ int64_t wls_smem[];
     const int y = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
     const size_t fo = (size_t)f * g.W * g.H;
     const int i = y - g.ry;
+    // border: this row's outputs outside the ROI (16 * (min_disp - 1)) are final now (the last FGS
+    // pass writes the ROI's)
+    if (border)
+        for (int x = tid; x < g.W; x += T)
+            if (i < 0 || i >= g.rh || x < g.rx || x >= g.rx + g.rw) wls_emit(wo, g, f, x, y, (int16_t)g.fill);
     if (i < 0 || i >= g.rh) {
         if (conf_full)
             for (int x = tid; x < g.W; x += T) conf_full[fo + (size_t)y * g.W + x] = 255.0f;
@@ -504,16 +547,30 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
     float* disc = (float*)(V + 2 * rw);    // [2][rw] discontinuity values
     const int16_t* L = dl + fo;
     const int16_t* R = dr + fo;
+    // the window's rows (wave-uniform: one image row per workgroup), then all 2(2r+1) loads of a
+    // column at once: RMAX taps unrolled, those past the radius loading a duplicate row and masked
+    // (a runtime-length tap loop issued its loads one iteration at a time)
+    size_t rowo[2 * RMAX + 1];
+#pragma unroll
+    for (int t = 0; t <= 2 * RMAX; t++)
+        rowo[t] = (size_t)(g.ry + reflect101(i + min(max(t - RMAX, -r), r), g.rh)) * g.W;
     for (int j = tid; j < rw; j += T) {
+        int vl[2 * RMAX + 1], vr[2 * RMAX + 1];
+#pragma unroll
+        for (int t = 0; t <= 2 * RMAX; t++) {
+            vl[t] = L[rowo[t] + g.rx + j];
+            vr[t] = R[rowo[t] + g.rrx + j];
+        }
         int s0 = 0, s1 = 0;
         int64_t q0 = 0, q1 = 0;
-        for (int a = -r; a <= r; a++) {
-            const size_t ro = (size_t)(g.ry + reflect101(i + a, g.rh)) * g.W;
-            const int vl = L[ro + g.rx + j], vr = R[ro + g.rrx + j];
-            s0 += vl;
-            q0 += (int64_t)vl * vl;
-            s1 += vr;
-            q1 += (int64_t)vr * vr;
+#pragma unroll
+        for (int t = 0; t <= 2 * RMAX; t++) {
+            const int a = t - RMAX;
+            const int ml = a >= -r && a <= r ? vl[t] : 0, mr = a >= -r && a <= r ? vr[t] : 0;
+            s0 += ml;
+            q0 += (int64_t)ml * ml;
+            s1 += mr;
+            q1 += (int64_t)mr * mr;
         }
         V[j] = s0;
         V[rw + j] = s1;
@@ -521,12 +578,18 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
         V2[rw + j] = q1;
     }
     __syncthreads();
+    // BORDER_REFLECT_101 of a column index one reflection deep (rw > RMAX; narrower ROIs loop)
+    const bool shallow = rw > RMAX;
+    auto refl = [&](int p) { return shallow ? (p < 0 ? -p : p >= rw ? 2 * rw - 2 - p : p) : reflect101(p, rw); };
     for (int j = tid; j < rw; j += T) {
 #pragma unroll
         for (int m = 0; m < 2; m++) {
             long long s = 0, s2 = 0;
-            for (int b = -r; b <= r; b++) {
-                const int jj = reflect101(j + b, rw);
+#pragma unroll
+            for (int t = 0; t <= 2 * RMAX; t++) {
+                const int b = t - RMAX;
+                if (b < -r || b > r) continue;  // uniform
+                const int jj = refl(j + b);
                 s += V[m * rw + jj];
                 s2 += V2[m * rw + jj];
             }
@@ -590,30 +653,17 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
 // (convertTo(CV_32F, 1/16)) and xyz = reprojectImageTo3D(fout, Q) (computeDepth,
 // handleMissing = false).
 __global__ __launch_bounds__(256) void k_wls_final(const float* __restrict__ A,
-                                                   const float* __restrict__ B, WlsGeom g,
-                                                   int16_t* __restrict__ out, float* __restrict__ fout,
-                                                   Q16 Q, float* __restrict__ xyz) {
+                                                   const float* __restrict__ B, WlsGeom g, WlsOut wo) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= g.W || y >= g.H) return;
-    const size_t o = (size_t)blockIdx.z * g.W * g.H + (size_t)y * g.W + x;
     const int j = x - g.rx, i = y - g.ry;
     int16_t r = (int16_t)g.fill;
     if (j >= 0 && j < g.rw && i >= 0 && i < g.rh) {
         const size_t co = (size_t)blockIdx.z * g.rw * g.rh + (size_t)i * g.rw + j;
-        const float c = B[co];
-        const float v = c != 0.0f ? A[co] / c : 0.0f;
-        // cvRound (cvtss2si): NaN / |v| >= 2^31 give INT_MIN, which saturates to -32768
-        float q = rintf(v);
-        q = fminf(fmaxf(q, -32768.0f), 32767.0f);
-        r = fabsf(v) < 2147483648.0f ? (int16_t)(int)q : (int16_t)-32768;
+        r = wls_value(A[co], B[co]);
     }
-    out[o] = r;
-    if (fout) {
-        const float df = (float)r * 0.0625f;
-        fout[o] = df;
-        if (xyz) reproject_px(Q, x, y, (double)df, 0.0, 0, xyz + 3 * o);
-    }
+    wls_emit(wo, g, blockIdx.z, x, y, r);
 }
 
 // FastGlobalSmootherFilter::filter on nimg (1 or 2) row-major w x h images per frame (R0, R1, in
@@ -631,9 +681,9 @@ static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const flo
 
 // k_fgs_pcr instance for G*n samples per block: one equation per thread up to 1024 samples
 // (T = the samples rounded up to whole waves), 2 or 4 per thread of 1024 beyond
-template <bool TWO>
+template <bool TWO, bool FIN = false>
 static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F, int rows,
-                      float lam, hipStream_t st) {
+                      float lam, hipStream_t st, const WlsGeom& gw = {}, const WlsOut& wo = {}) {
     const int n = rows ? w : h, nlines = rows ? h : w;
     if (n > kPcrMaxN) return -1;
     // short lines: G per block so that a block holds up to 1024 samples
@@ -655,14 +705,17 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
     const bool db = (size_t)N * 48 <= (size_t)max_lds;
     if (!db && (size_t)N * 24 > (size_t)max_lds) return -1;
     if (!db) {
-        hipLaunchKernelGGL((k_fgs_pcr<4, TWO, false>), grid, blk, (size_t)N * 24, st, U0, U1, Cw, w, h, fs, rows,
-                           G, lam);
+        hipLaunchKernelGGL((k_fgs_pcr<4, TWO, false, FIN>), grid, blk, (size_t)N * 24, st, U0, U1, Cw, w, h, fs,
+                           rows, G, lam, gw, wo);
         return 0;
     }
     const size_t lds = (size_t)N * 48;
-    if (ept == 1) hipLaunchKernelGGL((k_fgs_pcr<1, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
-    else if (ept == 2) hipLaunchKernelGGL((k_fgs_pcr<2, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
-    else hipLaunchKernelGGL((k_fgs_pcr<4, TWO>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam);
+    if (ept == 1)
+        hipLaunchKernelGGL((k_fgs_pcr<1, TWO, true, FIN>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam, gw, wo);
+    else if (ept == 2)
+        hipLaunchKernelGGL((k_fgs_pcr<2, TWO, true, FIN>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam, gw, wo);
+    else
+        hipLaunchKernelGGL((k_fgs_pcr<4, TWO, true, FIN>), grid, blk, lds, st, U0, U1, Cw, w, h, fs, rows, G, lam, gw, wo);
     return 0;
 }
 
@@ -676,7 +729,8 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
 static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
                       int iters, int solver, const FgsScratch& s, hipStream_t st,
-                      bool weights_ready = false, sdr_sgbm* timer = nullptr) {
+                      bool weights_ready = false, sdr_sgbm* timer = nullptr,
+                      const WlsGeom* fin_g = nullptr, const WlsOut* fin_o = nullptr) {
     const size_t fs = (size_t)w * h;
     const bool pcr = solver == SDR_FGS_PCR;
     if (!weights_ready)
@@ -695,8 +749,12 @@ static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, con
             }
             {
                 KScope kt(timer, SDR_KERNEL_FGS);
-                e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
-                        : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
+                // the last column pass writes the filter's outputs itself (fin_g / fin_o)
+                if (fin_g && R1 && it == iters - 1)
+                    e2 = launch_pcr<true, true>(R0, R1, s.Cv, w, h, F, 0, lam, st, *fin_g, *fin_o);
+                else
+                    e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
+                            : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
             }
             if (e1 || e2) return -1;
         } else {
@@ -900,7 +958,7 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     if (roi && p.fgs_solver == SDR_FGS_PCR && (g.rw > sdr::kPcrMaxN || g.rh > sdr::kPcrMaxN))
         return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                             "(use SDR_FGS_THOMAS for larger ROIs)");
-    const bool fused = roi && g.rw <= sdr::kPcrMaxN;
+    const bool fused = roi && g.rw <= sdr::kPcrMaxN && g.radius <= 9;
     const size_t cpx = roi ? (size_t)g.rw * g.rh : 0;
     int rc;
     const float* lut = nullptr;
@@ -916,11 +974,24 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     const dim3 blk(256);
     const bool rowmajor = p.fgs_solver == SDR_FGS_PCR;
     const dim3 grid((W + 63) / 64, (H + 3) / 4, F);
+    sdr::WlsOut wo{out, fout, xyz, {}};
+    if (Q)
+        for (int t = 0; t < 16; t++) wo.Q.q[t] = Q[t];
+    // with the default solver the outputs need no pass of their own: k_wls_prep writes the pixels
+    // outside the ROI and the last FGS column pass the ROI's (k_wls_final otherwise)
+    const bool fin_fused = fused && roi && p.fgs_solver == SDR_FGS_PCR;
     if (fused) {
         sdr::KScope kt(timer, SDR_KERNEL_WLS_PREP);
-        hipLaunchKernelGGL(sdr::k_wls_prep, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
-                           gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
-                           (float*)h->Cv.p);
+        // the window radius is ceil(blockSize / 2) <= 9 for every valid SGBM block; wider ones
+        // (setDepthDiscontinuityRadius) take the per-pixel kernels below
+        if (g.radius <= 4)
+            hipLaunchKernelGGL(sdr::k_wls_prep<4>, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
+                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
+                               (float*)h->Cv.p, fin_fused ? 1 : 0, wo);
+        else
+            hipLaunchKernelGGL(sdr::k_wls_prep<9>, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
+                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
+                               (float*)h->Cv.p, fin_fused ? 1 : 0, wo);
     } else {
         sdr::KScope kt(timer, SDR_KERNEL_WLS_PREP);
         if (roi)
@@ -934,16 +1005,18 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
         const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
                                  (float*)h->Cv.p};
         if (sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
-                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused, timer))
+                            p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused, timer,
+                            fin_fused ? &g : nullptr, fin_fused ? &wo : nullptr))
             return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                                 "(use SDR_FGS_THOMAS for larger ROIs)");
+        if (fin_fused) {
+            WLS_HIP(hipGetLastError());
+            return SDR_OK;
+        }
     }
-    sdr::Q16 q{};
-    if (Q)
-        for (int t = 0; t < 16; t++) q.q[t] = Q[t];
     {
         sdr::KScope kt(timer, SDR_KERNEL_WLS_FINAL);
-        hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, out, fout, q, xyz);
+        hipLaunchKernelGGL(sdr::k_wls_final, grid, blk, 0, st, A, B, g, wo);
     }
     WLS_HIP(hipGetLastError());
     return SDR_OK;

@@ -540,3 +540,29 @@ def test_graph_capture_compute_reproject(oracle):
         ref_xyz = oracle.reproject(oracle.disp_to_float(ref), S.REFERENCE_Q, True)
         assert np.array_equal(xyz[0].cpu().numpy().view(np.uint32), ref_xyz.view(np.uint32)), seed
     m.close()
+
+
+@pytest.mark.parametrize("mode,D,H,W,seed,batch", [
+    (2, 80, 601, 701, 31, 1),     # 3WAY, padded lanes (D < 128), odd row and column chain counts
+                                  # (one-chain last waves / workgroups)
+    (2, 128, 576, 800, 32, 1),    # 3WAY at D = 128 (no padding)
+    (3, 64, 520, 600, 33, 1),     # MODE_HH4: E, W and N chains
+    (2, 48, 300, 420, 34, 4),     # a batch: 4 x 600 chains
+])
+def test_two_chain_paths(oracle, mode, D, H, W, seed, batch):
+    """k_paths with two chains per wave (launches of E/W/N chains with more chains than SIMDs, D <=
+    128: the class path's paired 640x360 matchers) and k_south_wta with two columns per workgroup
+    (more than 8 x CUs column chains: the 3WAY cases here) against the oracle, frame by frame."""
+    args = (0, D, 5, 600, 2400, 1, 63, 10, 0, 2, mode)
+    Ls = np.empty((batch, H, W), np.uint8)
+    Rs = np.empty((batch, H, W), np.uint8)
+    for i in range(batch):
+        Ls[i], Rs[i], _ = S.make_pair(H, W, D, seed=seed + i)
+    dev = torch.device("cuda", 0)
+    m = sdr.StereoSGBM.create(*args)
+    out = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    for i in range(batch):
+        ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
+        assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
+    m.close()

@@ -432,6 +432,10 @@ def main():
         el = max(r.pop("_s") for r in per_rank)
         ranks = {"backend": "gloo" if gloo else "nccl (RCCL)", "world_size_seen": dist.get_world_size(),
                  "per_rank": per_rank}
+    # a batched MODE_HH step whose row sweep gave up waiting wrote INVALID frames and reports it
+    # here (sdr_sgbm_last_status): such a run has no valid number
+    for mm in ms:
+        mm.check_status()
     gather_check = None
     if world > 1:
         # end-to-end check of the data path (after the timed region): rank 0's copy of every rank's

@@ -258,7 +258,8 @@ def main():
     if env_world is None and a.gpus > 1:
         # no launcher: start the N ranks from here, before anything initialises HIP (this process
         # imports no torch; the ranks are fresh child processes)
-        sys.exit(relay(launcher_cmd(a.gpus, free_port(), sys.argv[1:]), a.gpus))
+        sys.exit(relay(launcher_cmd(a.gpus, free_port(), sys.argv[1:]), a.gpus,
+                       env=dict(os.environ, SDR_BENCH_SELF_LAUNCHED="1")))
     world = int(env_world or "1")
     if world != a.gpus:
         raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}: the launcher and the "
@@ -431,6 +432,8 @@ def main():
                                           "ms_per_step": round(el / a.steps * 1e3, 4), "_s": el})
         el = max(r.pop("_s") for r in per_rank)
         ranks = {"backend": "gloo" if gloo else "nccl (RCCL)", "world_size_seen": dist.get_world_size(),
+                 "launcher": ("bench.py --gpus (torch.distributed.run child)"
+                              if os.environ.get("SDR_BENCH_SELF_LAUNCHED") else "external"),
                  "per_rank": per_rank}
     # a batched MODE_HH step whose row sweep gave up waiting wrote INVALID frames and reports it
     # here (sdr_sgbm_last_status): such a run has no valid number

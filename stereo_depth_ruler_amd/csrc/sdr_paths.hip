@@ -253,13 +253,13 @@ __device__ __forceinline__ Regs<2> path_step_tc(Regs<2> c, Regs<2>& Lp, uint32_t
         L.r[i] = l;
         m = pk_min(m, l);
     }
-    // the two chains' minima: 16-lane rows, then rows 0+1 and 2+3 (row_bcast:15 into rows 1, 3)
+    // the two chains' minima, in every lane of each half: 16-lane row minima (DPP), then rows 0+1
+    // and 2+3 by one v_permlane16_swap (rows 0 <-> 1, 2 <-> 3); no readlane / scalar round trip
     uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu), (unsigned short)(m >> 16));
     m16 = row16_min_u32(m16);
-    m16 = min(m16, (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m16, 0x142, 0xa, 0xf, false));
-    const uint32_t dA = (uint32_t)__builtin_amdgcn_readlane((int)m16, 31) * 0x00010001u + P2x2;
-    const uint32_t dB = (uint32_t)__builtin_amdgcn_readlane((int)m16, 63) * 0x00010001u + P2x2;
-    delta2 = lane >= 32 ? dB : dA;
+    const auto p16 = __builtin_amdgcn_permlane16_swap(m16, m16, false, false);
+    m16 = min((uint32_t)p16[0], (uint32_t)p16[1]);
+    delta2 = m16 * 0x00010001u + P2x2;
     Lp = L;
     return L;
 }
@@ -778,7 +778,10 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     constexpr int LSTR = DMAX / 2 + 4;  // dwords per staged row (padded: rows of a wave's 4 pixels)
     // consumer prefetch distance in blocks (= ring slots) of the other directions' L
     // (two blocks while the ring fits 64 VGPRs; 1 block -- a ring of 56 VGPRs -- for 8 paths at D > 128)
-    constexpr int PD = NP * WK * kSouthRPW * NCOL <= 128 ? 2 : 1;
+#ifndef SDR_SOUTH_TC_PD
+#define SDR_SOUTH_TC_PD 2
+#endif
+    constexpr int PD = TC ? SDR_SOUTH_TC_PD : NP * WK * kSouthRPW <= 128 ? 2 : 1;
     static_assert((PD + 1) * RB <= kSouthPad, "consumer load overrun must fit the row slack");
     __shared__ uint32_t sL[2][RB][NCOL][LSTR];
     // each consumer row's S staged for the subpixel neighbours and the uniqueness minimum (one

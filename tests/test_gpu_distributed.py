@@ -130,6 +130,7 @@ def test_bench_gpus2_self_launch():
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert out["gather_check"]["ok"] and out["gather_check"]["ranks"] == 2
     assert out["ranks"]["world_size_seen"] == 2 and len(out["ranks"]["per_rank"]) == 2
+    assert out["ranks"]["launcher"].startswith("bench.py --gpus")
     assert {r["rank"] for r in out["ranks"]["per_rank"]} == {0, 1}
     worst = max(r["ms_per_step"] for r in out["ranks"]["per_rank"])
     assert abs(out["ms_per_step"] - worst) < 1e-3 + 1e-3 * worst

@@ -170,6 +170,24 @@ def test_wls_params_variants(oracle, solver):
         assert np.array_equal(got, ref), (minD, numD, bs)
 
 
+@pytest.mark.parametrize("radius", [1, 4, 5, 9, 10])
+def test_wls_radius_paths(oracle, radius):
+    """setDepthDiscontinuityRadius across the front end's paths: k_wls_prep with 4 (r <= 4) or 9
+    (r <= 9) taps unrolled, and past 9 the per-pixel kernels with k_wls_final; with the default
+    solver the first two write the outputs outside the ROI in k_wls_prep and the ROI's in the last
+    FGS pass, the third in k_wls_final."""
+    h, w = 61, 150
+    L, dl, dr = sgbm_pair_maps(oracle, h, w, 32, 40 + radius)
+    q = oracle.wls_params_for_sgbm(0, 32, 5, w, h, 8000.0, 1.1)
+    q.depth_disc_radius = radius
+    q.roi_y, q.roi_h = 2, h - 5
+    ref, ref_conf = oracle.wls_filter(dl, dr, L, q, return_conf=True)
+    f = make_filter(q, w, h)
+    got = f.filter(dl, L, dr)
+    assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf))
+    assert np.array_equal(got, ref), (got != ref).sum()
+
+
 @pytest.mark.parametrize("solver", SOLVERS)
 def test_wls_edge_cases(oracle, solver):
     h, w = 40, 120

@@ -294,6 +294,10 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    if os.environ.get("SDR_BENCH_LIB"):
+        # experiment A/B only: time another build of the engine (scripts/; never the driver's run)
+        from stereo_depth_ruler_amd import _lib as _l
+        _l.use_library(os.environ["SDR_BENCH_LIB"])
     import stereo_depth_ruler_amd as sdr
     from stereo_depth_ruler_amd import synthetic as S
     from stereo_depth_ruler_amd.distributed import as_bytes

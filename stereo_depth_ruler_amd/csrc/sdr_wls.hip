@@ -383,7 +383,10 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
     }
     __syncthreads();
     int buf = 0;
-    for (int s = 1; s < n; s <<= 1, buf ^= DB ? N : 0) {
+#ifndef SDR_PCR_PROBE
+#define SDR_PCR_PROBE 0  // timing probes only (wrong results): 1 = no stages, 2 = rcp for the division
+#endif
+    for (int s = 1; s < (SDR_PCR_PROBE == 1 ? 1 : n); s <<= 1, buf ^= DB ? N : 0) {
         float4* Xb = X + buf;
         float* Ab = A + buf;
         float* Cb = Cc + buf;
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * T;
             if (e < N) {
-                Xb[e] = make_float4(rs[j], 1.0f / b[j], d0[j], d1[j]);
+                Xb[e] = make_float4(rs[j], SDR_PCR_PROBE == 2 ? __builtin_amdgcn_rcpf(b[j]) : 1.0f / b[j], d0[j], d1[j]);
                 Ab[e] = a[j];
                 Cb[e] = c[j];
             }

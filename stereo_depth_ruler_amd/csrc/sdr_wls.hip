@@ -692,7 +692,10 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
     // short lines: G per block so that a block holds up to 1024 samples
     const int G = std::max(1, std::min(nlines, 1024 / n));
     const int N = G * n;
-    const int ept = N <= 1024 ? 1 : N <= 2048 ? 2 : 4;
+#ifndef SDR_PCR_EPT_MIN
+#define SDR_PCR_EPT_MIN 1
+#endif
+    const int ept = std::max(SDR_PCR_EPT_MIN, N <= 1024 ? 1 : N <= 2048 ? 2 : 4);
     const int T = std::min(1024, ((N + ept - 1) / ept + 63) / 64 * 64);
     const dim3 grid((nlines + G - 1) / G, F), blk(T);
     const size_t fs = (size_t)w * h;

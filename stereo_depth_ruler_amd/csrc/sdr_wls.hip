@@ -383,10 +383,7 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
     }
     __syncthreads();
     int buf = 0;
-#ifndef SDR_PCR_PROBE
-#define SDR_PCR_PROBE 0  // timing probes only (wrong results): 1 = no stages, 2 = rcp for the division
-#endif
-    for (int s = 1; s < (SDR_PCR_PROBE == 1 ? 1 : n); s <<= 1, buf ^= DB ? N : 0) {
+    for (int s = 1; s < n; s <<= 1, buf ^= DB ? N : 0) {
         float4* Xb = X + buf;
         float* Ab = A + buf;
         float* Cb = Cc + buf;
@@ -394,7 +391,7 @@ __global__ __launch_bounds__(1024) void k_fgs_pcr(float* U0, float* U1, const fl
         for (int j = 0; j < EPT; j++) {
             const int e = tid + j * T;
             if (e < N) {
-                Xb[e] = make_float4(rs[j], SDR_PCR_PROBE == 2 ? __builtin_amdgcn_rcpf(b[j]) : 1.0f / b[j], d0[j], d1[j]);
+                Xb[e] = make_float4(rs[j], 1.0f / b[j], d0[j], d1[j]);
                 Ab[e] = a[j];
                 Cb[e] = c[j];
             }
@@ -692,10 +689,8 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
     // short lines: G per block so that a block holds up to 1024 samples
     const int G = std::max(1, std::min(nlines, 1024 / n));
     const int N = G * n;
-#ifndef SDR_PCR_EPT_MIN
-#define SDR_PCR_EPT_MIN 1
-#endif
-    const int ept = std::max(SDR_PCR_EPT_MIN, N <= 1024 ? 1 : N <= 2048 ? 2 : 4);
+    // (one equation per thread: 2 or 4 per thread at 640x360 measured 12.8 -> 15.0 / 16.8 us a pass)
+    const int ept = N <= 1024 ? 1 : N <= 2048 ? 2 : 4;
     const int T = std::min(1024, ((N + ept - 1) / ept + 63) / 64 * 64);
     const dim3 grid((nlines + G - 1) / G, F), blk(T);
     const size_t fs = (size_t)w * h;

@@ -502,7 +502,8 @@ def main():
         avg_s = tot_ms / cnt / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
         label = {
-            "k_paths": f"k_paths<DPL={2 if D <= 128 else 4}> ({kp_dirs} of the {P} path directions of a batch in "
+            "k_paths": f"k_paths<DPL={2 if D <= 128 else 4}> or k_paths_tc (two chains per wave, the engine's pick "
+                       f"for latency-bound launches) ({kp_dirs} of the {P} path directions of a batch in "
                        f"one launch; the top-to-bottom one is fused into k_south_wta)",
             "k_sweep": "k_sweep (row-synchronous up/down passes of batched MODE_HH)",
             "k_south_wta": f"k_south_wta (top-to-bottom path fused with the WTA, reading {nrec} records)",
@@ -514,7 +515,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(f"{a.config}:{name}"),
+            "traffic": load_traffic(f"{a.config}:{name}") or load_traffic(f"{a.config}:{name}_tc"),
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "bytes_model": f"{model}; cells={'2 matchers*' if nmatch == 2 else ''}batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),

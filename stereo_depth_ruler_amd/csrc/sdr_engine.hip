@@ -355,6 +355,14 @@ struct sdr_sgbm {
 };
 
 namespace {
+// Events that only order streams on this device (the handle's retire event, the sweep
+// serialisation, the class path's fork / join) and the per-kernel timers: a device-scope release.
+// The default event's system-scope release writes back and invalidates the caches at every record:
+// on the class path's frame that was a ~5 us idle gap between the matchers and the WLS filter, and
+// the kernels after it started on cold caches.  (The host-staging events of drain() keep the
+// default: the host reads what they order.)
+constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+constexpr unsigned kTimerEvent = hipEventReleaseToDevice;
 // A stream being captured into a graph (hipStreamBeginCapture, torch.cuda.graph).
 bool capturing(hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -384,8 +392,8 @@ bool sdr::ktimer_begin(sdr_sgbm* h, int kind) {
     if (h->timing < 2) return false;
     if (h->kused * 2 + 2 > h->kev.size()) {
         hipEvent_t a = nullptr, b = nullptr;
-        if (hipEventCreate(&a) != hipSuccess) return false;
-        if (hipEventCreate(&b) != hipSuccess) {
+        if (hipEventCreateWithFlags(&a, kTimerEvent) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&b, kTimerEvent) != hipSuccess) {
             (void)hipEventDestroy(a);
             return false;
         }
@@ -462,7 +470,8 @@ static bool can_pair(const Eff& a, const Eff& b) {
 
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
-                           int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr) {
+                           int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr,
+                           bool retire_after = true) {
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
@@ -700,7 +709,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         std::lock_guard<std::mutex> lk(g_sweep_mu);
         hipEvent_t& last = g_sweep_last[h->device];
         if (last) SDR_HIP(hipStreamWaitEvent(st, last, 0));
-        else SDR_HIP(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+        else SDR_HIP(hipEventCreateWithFlags(&last, kOrderEvent));
         for (int up = 1; up >= 0; up--) {
             sa.up = up;
             sa.ntiles = shp[up].ntiles;
@@ -749,7 +758,9 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         SDR_HIP(hipMemcpyAsync(h->status_host, h->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
-    retire(h);
+    // (the class path retires once, after its filter: every event record is a queue barrier, measured
+    // as a ~5.6 us idle gap between the matchers and the filter)
+    if (retire_after) retire(h);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -805,8 +816,8 @@ int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out) {
         return fail(SDR_ERR_DEVICE, "hipStreamCreate failed");
     }
     h->stream = h->own_stream;
-    for (auto& ev : h->ev) (void)hipEventCreate(&ev);
-    (void)hipEventCreateWithFlags(&h->done, hipEventDisableTiming);
+    for (auto& ev : h->ev) (void)hipEventCreateWithFlags(&ev, kTimerEvent);
+    (void)hipEventCreateWithFlags(&h->done, kOrderEvent);
     *out = h;
     return SDR_OK;
 }
@@ -1225,19 +1236,19 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
                  can_pair(el, er);
     }
     if (paired) {
-        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, 2 * F, dl, nullptr, &fin, 1, &right->p)))
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, 2 * F, dl, nullptr, &fin, 1, &right->p, false)))
             return rc;
     } else if (right) {
         if (!left->side) {
             SDR_HIP(hipStreamCreateWithFlags(&left->side, hipStreamNonBlocking));
-            SDR_HIP(hipEventCreateWithFlags(&left->fork, hipEventDisableTiming));
-            SDR_HIP(hipEventCreateWithFlags(&left->join, hipEventDisableTiming));
+            SDR_HIP(hipEventCreateWithFlags(&left->fork, kOrderEvent));
+            SDR_HIP(hipEventCreateWithFlags(&left->join, kOrderEvent));
         }
         SDR_HIP(hipEventRecord(left->fork, st));
         SDR_HIP(hipStreamWaitEvent(left->side, left->fork, 0));
         hipStream_t rs = right->stream;
         if ((rc = use_stream(right, left->side))) return rc;
-        rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
+        rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin, 1, nullptr, false);
         retire(right);
         const int rc2 = use_stream(right, rs);
         if (rc) return rc;
@@ -1245,7 +1256,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
     if (!paired) {
-        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin, 1, nullptr, false))) return rc;
         if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
     }
     if (wls) {

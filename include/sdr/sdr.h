@@ -85,7 +85,9 @@ int sdr_sgbm_destroy(sdr_sgbm* h);
 int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p);
 int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p);
 /* HIP stream (hipStream_t) the handle launches on (NULL = the HIP null stream, e.g. torch's
- * default stream); a new handle uses a stream of its own, restored by sdr_sgbm_reset_stream. */
+ * default stream); a new handle uses a stream of its own, restored by sdr_sgbm_reset_stream.
+ * Changing the stream orders the handle's pending work on the previous stream before the new
+ * stream's (an event recorded there at the switch), so the previous stream must still exist. */
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
 int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);

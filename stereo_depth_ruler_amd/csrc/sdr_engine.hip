@@ -368,21 +368,23 @@ bool capturing(hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
-// The handle's last enqueue, for the next stream that uses its scratch.  Not recorded into a
-// graph capture: the capture's replays order themselves.
-void retire(sdr_sgbm* h) {
-    if (!h->done) return;
-    if (capturing(h->stream)) {
-        h->pending = false;
-        return;
-    }
-    if (hipEventRecord(h->done, h->stream) == hipSuccess) h->pending = true;
-}
+// The handle's last enqueue, for the next stream that uses its scratch.  Recorded lazily: only
+// when the handle moves to another stream does its old stream get the event (after everything
+// queued there so far, the handle's work included), and the new stream wait on it.  An event
+// record is a queue barrier: recorded after every call it left a ~5.4 us idle gap per class-path
+// frame.  Hence the previous stream must still exist when the handle changes streams (as it must
+// for sdr_sgbm_destroy's synchronisation).  Nothing is recorded into or waited on from a graph
+// capture: the capture's replays order themselves.
+void retire(sdr_sgbm* h) { h->pending = true; }
 int use_stream(sdr_sgbm* h, hipStream_t s) {
     // a stream being captured neither queries nor waits on an event recorded outside the capture
     // (both invalidate a global-mode capture); torch.cuda.graph synchronises before it captures,
     // and a caller capturing by hand orders the handle's earlier work before the capture itself
-    if (s != h->stream && h->pending && !capturing(s)) SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
+    if (s != h->stream && h->pending && h->done && !capturing(h->stream) && !capturing(s)) {
+        SDR_HIP(hipEventRecord(h->done, h->stream));
+        SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
+    }
+    if (s != h->stream) h->pending = false;
     h->stream = s;
     return SDR_OK;
 }
@@ -470,8 +472,7 @@ static bool can_pair(const Eff& a, const Eff& b) {
 
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
-                           int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr,
-                           bool retire_after = true) {
+                           int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr) {
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
@@ -758,9 +759,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         SDR_HIP(hipMemcpyAsync(h->status_host, h->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
-    // (the class path retires once, after its filter: every event record is a queue barrier, measured
-    // as a ~5.6 us idle gap between the matchers and the filter)
-    if (retire_after) retire(h);
+    retire(h);
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -1236,7 +1235,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
                  can_pair(el, er);
     }
     if (paired) {
-        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, 2 * F, dl, nullptr, &fin, 1, &right->p, false)))
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, 2 * F, dl, nullptr, &fin, 1, &right->p)))
             return rc;
     } else if (right) {
         if (!left->side) {
@@ -1248,7 +1247,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         SDR_HIP(hipStreamWaitEvent(left->side, left->fork, 0));
         hipStream_t rs = right->stream;
         if ((rc = use_stream(right, left->side))) return rc;
-        rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin, 1, nullptr, false);
+        rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
         retire(right);
         const int rc2 = use_stream(right, rs);
         if (rc) return rc;
@@ -1256,7 +1255,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
     if (!paired) {
-        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin, 1, nullptr, false))) return rc;
+        if ((rc = enqueue_compute(left, sl, sr, w2, h2, w2, px2, F, dl, nullptr, &fin))) return rc;
         if (right) SDR_HIP(hipStreamWaitEvent(st, left->join, 0));
     }
     if (wls) {

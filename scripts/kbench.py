@@ -26,8 +26,11 @@ CONFIGS = {  # W, H, D, mode, frames
     "c0": (640, 360, 80, 2, 1),
     "c5": (1920, 1080, 256, 1, 1),
     "c4": (640, 360, 80, 2, 2),  # the class path's two matchers as two frames (1440 E/W chains)
+    "c5b8": (1920, 1080, 256, 1, 8),  # C5 as benched: 8 frames through the row sweeps
+    "hh128": (1280, 720, 128, 1, 8),  # the sweeps at two disparities per lane
 }
-KINDS = ["prefilter", "k_cost", "k_paths", "k_south_wta", "median", "speckle", "reproject", "k_lr_check"]
+KINDS = ["prefilter", "k_cost", "k_paths", "k_south_wta", "median", "speckle", "reproject", "k_lr_check",
+         "k_sweep"]  # SDR_KERNEL_* order
 
 
 def load(path):

@@ -98,6 +98,65 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
     return L;
 }
 
+// The recurrence of one step without its wave minimum: returns L and leaves the lane's minimum
+// over its pairs (low half) in m16, for callers that reduce several chains' minima together
+// (k_sweep, wave_deltas: interleaved, so the DPP steps' wait states overlap).
+template <int K, bool PAD>
+__device__ __forceinline__ Regs<K> path_step_min16(Regs<K> c, const Regs<K>& Lp, uint32_t delta2, uint32_t P1x2,
+                                                   bool active, uint32_t& upr, uint32_t& dnr, uint32_t& m16) {
+    if constexpr (PAD) {
+#pragma unroll
+        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
+    }
+    const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
+    const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
+    Regs<K> L;
+    uint32_t m = kMaxPair;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
+        const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
+        uint32_t t = pk_add_sat(pk_min(dm1, dp1), P1x2);
+        t = pk_min(pk_min(t, Lp.r[i]), delta2);
+        uint32_t l = pk_sub(pk_add(c.r[i], t), delta2);
+        if constexpr (PAD) l = active ? l : kMaxPair;
+        L.r[i] = l;
+        m = pk_min(m, l);
+    }
+    m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu), (unsigned short)(m >> 16));
+    return L;
+}
+
+// N wave-uniform minima (wave_min_u32_uniform's steps) reduced together, step by step: each DPP
+// step of one value is N-1 instructions after the previous one, past the 2-wait-state VALU ->
+// DPP read hazard that a single reduction pays as an s_nop per step.  Returns min * 0x10001 + P2.
+template <int N>
+__device__ __forceinline__ void wave_deltas(uint32_t (&m)[N], uint32_t (&delta2)[N], uint32_t P2x2) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppQuadXor1>(m[i]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppQuadXor2>(m[i]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppRowHalfMirror>(m[i]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppRowMirror>(m[i]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        m[i] = min(m[i], (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m[i], 0x142, 0xa, 0xf, false));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        m[i] = min(m[i], (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m[i], 0x143, 0xc, 0xf, false));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < N; i++) delta2[i] = (uint32_t)__builtin_amdgcn_readlane((int)m[i], 63) * 0x00010001u + P2x2;
+}
+
 // k_paths lookahead (steps).  32 steps at D <= 128 measured slower on the class path's 640x360
 // frames (k_paths 75 -> 82 us for both matchers; C2 unchanged): its E/W chains wait on the
 // memory system (3.4 TB/s over the launch), not on the lookahead.
@@ -422,6 +481,12 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
     constexpr int K = DPL / 2, NC = sweep_cols(DPL, UP), NWV = kSweepWaves, NO = kSweepOwn, RS = NC - 1;
     constexpr int TILE = NC * NO;
     static_assert(RS < NC, "a halo of NC columns feeds the tile exact values for NC - 1 rows");
+    // the row's wave minima reduced together (wave_deltas) except where their registers would
+    // spill (the padded D = 144..240 down pass: 168 VGPRs and 16 B of scratch a lane)
+#ifndef SDR_SWEEP_BATCH
+#define SDR_SWEEP_BATCH 1
+#endif
+    constexpr bool BATCH = SDR_SWEEP_BATCH && !(PAD && DPL == 4 && !UP);
     constexpr int RING = 2;  // cost rows in registers: row k in slot k % 2, loaded a row (~2 us) ahead
     __shared__ uint32_t xA[2][NWV][64 * K];  // row parity, wave: diagonal A of its last column
     __shared__ uint32_t xB[2][NWV][64 * K];  // diagonal B of its first column
@@ -555,27 +620,37 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
             uint32_t doutA = P2x2, doutB = P2x2;
             // diagonal A over the columns, from the column on the left (inA: the wave to the left,
             // through LDS); descending, so La[j-1] is still the previous row's when column j takes it
+            // (BATCH: the columns' wave minima are reduced together after the loop, wave_deltas)
             auto diag_a = [&](const Regs<K>& inA, uint32_t dinA, Regs<K>* sum) __attribute__((always_inline)) {
+                uint32_t m16[NC];
 #pragma unroll
                 for (int j = NC - 1; j >= 0; j--) {
                     Regs<K> p = j > 0 ? La[j > 0 ? j - 1 : 0] : inA;
                     uint32_t dp = j > 0 ? da[j > 0 ? j - 1 : 0] : dinA;
                     uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    const Regs<K> L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                    Regs<K> L;
+                    if constexpr (BATCH) {
+                        L = path_step_min16<K, PAD>(c[j], p, dp, P1x2, active, upr, dnr, m16[j]);
+                    } else {
+                        L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                        da[j] = dp;
+                    }
                     La[j] = L;
-                    da[j] = dp;
                     const bool o = j == ncol - 1;
 #pragma unroll
                     for (int i = 0; i < K; i++) outA.r[i] = o ? L.r[i] : outA.r[i];
-                    doutA = o ? dp : doutA;
                     if (sum) {
 #pragma unroll
                         for (int i = 0; i < K; i++) sum[j].r[i] = UP ? pk_add_sat(sum[j].r[i], L.r[i]) : L.r[i];
                     }
                 }
+                if constexpr (BATCH) wave_deltas<NC>(m16, da, P2x2);
+#pragma unroll
+                for (int j = 0; j < NC; j++) doutA = j == ncol - 1 ? da[j] : doutA;
             };
             // diagonal B from the column on the right (inB past the wave's last valid column)
             auto diag_b = [&](const Regs<K>& inB, uint32_t dinB, Regs<K>* sum) __attribute__((always_inline)) {
+                uint32_t m16[NC];
 #pragma unroll
                 for (int j = 0; j < NC; j++) {
                     const bool in = j + 1 < ncol;
@@ -584,14 +659,20 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
                     for (int i = 0; i < K; i++) p.r[i] = in ? Lb[j + 1 < NC ? j + 1 : NC - 1].r[i] : inB.r[i];
                     uint32_t dp = in ? db[j + 1 < NC ? j + 1 : NC - 1] : dinB;
                     uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    const Regs<K> L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                    Regs<K> L;
+                    if constexpr (BATCH) {
+                        L = path_step_min16<K, PAD>(c[j], p, dp, P1x2, active, upr, dnr, m16[j]);
+                    } else {
+                        L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
+                        db[j] = dp;
+                    }
                     Lb[j] = L;
-                    db[j] = dp;
                     if (sum) {
 #pragma unroll
                         for (int i = 0; i < K; i++) sum[j].r[i] = pk_add_sat(sum[j].r[i], L.r[i]);
                     }
                 }
+                if constexpr (BATCH) wave_deltas<NC>(m16, db, P2x2);
                 outB = Lb[0];
                 doutB = db[0];
             };
@@ -612,11 +693,16 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArg
                 }
                 Regs<K> sum[NC];
                 if constexpr (UP) {
+                    uint32_t m16[NC];
 #pragma unroll
                     for (int j = 0; j < NC; j++) {
                         uint32_t upr = kMaxPair, dnr = kMaxPair;
-                        sum[j] = path_step<K, PAD, true>(c[j], Lv[j], dv[j], P1x2, P2x2, active, upr, dnr);
+                        if constexpr (BATCH)
+                            sum[j] = Lv[j] = path_step_min16<K, PAD>(c[j], Lv[j], dv[j], P1x2, active, upr, dnr, m16[j]);
+                        else
+                            sum[j] = path_step<K, PAD, true>(c[j], Lv[j], dv[j], P1x2, P2x2, active, upr, dnr);
                     }
+                    if constexpr (BATCH) wave_deltas<NC>(m16, dv, P2x2);
                 }
                 diag_a(inA, dinA, sum);
                 diag_b(inB, dinB, sum);

@@ -58,26 +58,15 @@ __device__ __forceinline__ Chain make_chain(const Geometry& g, const PathDir& d,
     return ch;
 }
 
-// One step of the path recurrence on a wave's packed int16 pairs (lane l: disparities
-// [l*2K, l*2K + 2K)); returns L of this pixel.  State: Lp := L, delta2 := minL + P2 (both
-// halves).  upr/dnr: the lane-shifted neighbour words of the previous step -- a wave shift leaves
-// the lane without a source (lane 0 / lane 63) unwritten, so passing the previous shift as the
-// DPP's old value keeps the kMaxPair boundary there from the first step on, with no refill.
-// (An offset-carrying form that takes the wave minimum off the serial chain was bit-exact and
-// not faster on MI355X; DESIGN.md 5.)
-// UNIFORM: the wave minimum as a scalar (k_paths: one chain per wave); false: broadcast in a VGPR
-// (k_sweep: dozens of chains per wave, whose deltas would not fit the SGPRs)
-template <int K, bool PAD, bool UNIFORM = true>
-__device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
-                                             uint32_t P2x2, bool active, uint32_t& upr, uint32_t& dnr) {
-    if constexpr (PAD) {
-#pragma unroll
-        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
-    }
-    const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
-    const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
-    Regs<K> L;
-    uint32_t m = kMaxPair;
+// The per-word recurrence of one step: L = C + min(Lp, min(Lp[d-1], Lp[d+1]) + P1, delta2) -
+// delta2 for the lane's K words, and m = the minimum of L's pairs.  (Issuing two words' packed ops
+// alternately -- 4 x int16 vector ops, no packed op right after the one it reads, so none of
+// gfx950's wait states -- removed ~40 % of the path kernels' s_nops and measured no faster: at
+// 3-4 waves per SIMD the other waves fill those slots; profiles/r4_ab_variants.txt.)
+template <int K, bool PAD>
+__device__ __forceinline__ void step_words(const Regs<K>& c, const Regs<K>& Lp, uint32_t delta2, uint32_t P1x2,
+                                           bool active, uint32_t up, uint32_t dn, Regs<K>& L, uint32_t& m) {
+    m = kMaxPair;
 #pragma unroll
     for (int i = 0; i < K; i++) {
         const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
@@ -89,6 +78,28 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
         L.r[i] = l;
         m = pk_min(m, l);
     }
+}
+
+// One step of the path recurrence on a wave's packed int16 pairs (lane l: disparities
+// [l*2K, l*2K + 2K)); returns L of this pixel.  State: Lp := L, delta2 := minL + P2 (both
+// halves).  upr/dnr: the lane-shifted neighbour words of the previous step -- a wave shift leaves
+// the lane without a source (lane 0 / lane 63) unwritten, so passing the previous shift as the
+// DPP's old value keeps the kMaxPair boundary there from the first step on, with no refill.
+// (An offset-carrying form that takes the wave minimum off the serial chain was bit-exact and
+// not faster on MI355X; DESIGN.md 5.)
+// UNIFORM: the wave minimum as a scalar (k_paths: one chain per wave); false: broadcast in a VGPR
+template <int K, bool PAD, bool UNIFORM = true>
+__device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
+                                             uint32_t P2x2, bool active, uint32_t& upr, uint32_t& dnr) {
+    if constexpr (PAD) {
+#pragma unroll
+        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
+    }
+    const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
+    const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
+    Regs<K> L;
+    uint32_t m;
+    step_words<K, PAD>(c, Lp, delta2, P1x2, active, up, dn, L, m);
     // min of the pair into the low half (one SDWA op; L >= 0, so u16 order is int16 order), the
     // wave minimum as a wave-uniform value, splatted and offset by P2 in scalar registers
     const uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu),
@@ -111,18 +122,8 @@ __device__ __forceinline__ Regs<K> path_step_min16(Regs<K> c, const Regs<K>& Lp,
     const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
     const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
     Regs<K> L;
-    uint32_t m = kMaxPair;
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        const uint32_t dm1 = funnel16(Lp.r[i], i == 0 ? up : Lp.r[i == 0 ? 0 : i - 1]);
-        const uint32_t dp1 = funnel16(i == K - 1 ? dn : Lp.r[i == K - 1 ? 0 : i + 1], Lp.r[i]);
-        uint32_t t = pk_add_sat(pk_min(dm1, dp1), P1x2);
-        t = pk_min(pk_min(t, Lp.r[i]), delta2);
-        uint32_t l = pk_sub(pk_add(c.r[i], t), delta2);
-        if constexpr (PAD) l = active ? l : kMaxPair;
-        L.r[i] = l;
-        m = pk_min(m, l);
-    }
+    uint32_t m;
+    step_words<K, PAD>(c, Lp, delta2, P1x2, active, up, dn, L, m);
     m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu), (unsigned short)(m >> 16));
     return L;
 }

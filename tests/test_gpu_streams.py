@@ -1,0 +1,61 @@
+"""One matcher moved between HIP streams while its earlier calls are still queued.
+
+A handle's scratch (cost volume, path records, ...) is reused by every call, so a call on a new
+stream must not start before the handle's work on the old stream is done.  The engine records its
+retire event on the old stream only at the switch (sdr_engine.hip use_stream; recording one per
+call was a queue barrier): these tests queue calls back to back across switches with
+no host synchronisation in between, and every output must equal the same call made alone.
+"""
+import numpy as np
+import pytest
+
+import stereo_depth_ruler_amd as sdr
+from stereo_depth_ruler_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _refs(m, L, R, F, n):
+    out = []
+    for k in range(n):
+        out.append(m.compute(L[k * F:(k + 1) * F], R[k * F:(k + 1) * F]).clone())
+        torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("mode,D,F", [(sdr.MODE_SGBM, 128, 4), (sdr.MODE_HH, 64, 8)])
+def test_stream_switch_with_pending_work(mode, D, F, oracle):
+    """C2-sized frames (a few ms of queued work per call) through streams a, b, a, then the
+    handle's own stream: each call's disparity equals the synchronised one-at-a-time run (and the
+    first frame equals the oracle).  MODE_HH with 8 frames takes the row-sweep path."""
+    H, W = (720, 1280) if mode == sdr.MODE_SGBM else (240, 640)
+    n = 4
+    Ls, Rs = S.make_batch(n * F, H, W, D, seed0=900)
+    dev = torch.device("cuda", 0)
+    L, R = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    args = (0, D, 5, 600, 2400, 1, 63, 12, 200, 2, mode)
+    m = sdr.StereoSGBM.create(*args)
+    refs = _refs(m, L, R, F, n)
+    a, b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    outs = [torch.empty((F, H, W), dtype=torch.int16, device=dev) for _ in range(n)]
+    torch.cuda.synchronize()
+    for k, s in enumerate((a, b, a, None)):
+        if s is None:
+            m.compute(L[k * F:(k + 1) * F], R[k * F:(k + 1) * F], disp=outs[k])
+        else:
+            with torch.cuda.stream(s):
+                m.compute(L[k * F:(k + 1) * F], R[k * F:(k + 1) * F], disp=outs[k])
+    torch.cuda.synchronize()
+    for k in range(n):
+        assert torch.equal(outs[k], refs[k]), k
+    p = oracle.make_params(*args)
+    assert np.array_equal(refs[0][0].cpu().numpy(), oracle.sgbm_compute(Ls[0], Rs[0], p))
+    m.close()

@@ -36,6 +36,9 @@ def _batch(kind, F, H, W, D, seed):
     ("textured", 8, 26, 260, 160, 20, 5),   # DPL 4 with padded lanes
     ("steps", 10, 20, 100, 32, 0, 6),
     ("textured", 8, 18, 192, 32, 0, 7),     # W1 = 160: whole tiles only (80 columns)
+    ("textured", 8, 24, 300, 128, 0, 8),    # DPL 2 without padded lanes
+    ("noise", 8, 20, 400, 256, 10, 9),      # DPL 4 without padded lanes (C3 / C5's D)
+    ("binary", 8, 16, 380, 256, 0, 10),     # the same at the int16 extremes
 ])
 def test_hh_sweep_batch_bit_exact(oracle, kind, F, H, W, D, speckle, seed):
     args = (0, D, 5, 600, 2400, 1, 63, 10, speckle, 2, sdr.MODE_HH)
@@ -130,3 +133,39 @@ def test_two_handles_two_streams_concurrent_sweeps(oracle):
     assert np.array_equal(outs[3][F - 1].cpu().numpy(), oracle.sgbm_compute(batches[3][0][F - 1], batches[3][1][F - 1], p))
     for m in ms + [one]:
         m.close()
+
+
+hypothesis = pytest.importorskip("hypothesis")
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@st.composite
+def sweep_cases(draw):
+    D = 16 * draw(st.integers(1, 16))  # both lane widths, padded and full
+    bs = draw(st.sampled_from([1, 3, 5, 7]))
+    return dict(kind=draw(st.sampled_from(["textured", "noise", "binary", "steps"])),
+                F=draw(st.integers(8, 11)), H=draw(st.integers(4, 28)),
+                W=D + bs // 2 + 1 + draw(st.integers(0, 258)), D=D,  # W1 > blockSize / 2
+                bs=bs, P1=draw(st.integers(1, 400)),
+                P2x=draw(st.integers(2, 8)), uniq=draw(st.sampled_from([0, 5, 15])),
+                ws=draw(st.sampled_from([0, 0, 20])), seed=draw(st.integers(0, 10**6)))
+
+
+@settings(max_examples=12, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(case=sweep_cases())
+def test_hh_sweep_hypothesis_bit_exact(oracle, case):
+    """Random batched MODE_HH shapes through the row sweeps (every lane width, partial tiles,
+    block sizes, penalties), each frame against the oracle."""
+    c = case
+    args = (0, c["D"], c["bs"], c["P1"], c["P1"] * c["P2x"], 1, 63, c["uniq"], c["ws"], 2, sdr.MODE_HH)
+    Ls, Rs = _batch(c["kind"], c["F"], c["H"], c["W"], c["D"], c["seed"])
+    dev = torch.device("cuda", 0)
+    m = sdr.StereoSGBM.create(*args)
+    out = m.compute(torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)).cpu().numpy()
+    p = oracle.make_params(*args)
+    for i in range(c["F"]):
+        ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
+        assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
+    m.close()

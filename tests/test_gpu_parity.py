@@ -566,3 +566,33 @@ def test_two_chain_paths(oracle, mode, D, H, W, seed, batch):
         ref = oracle.sgbm_compute(Ls[i], Rs[i], p)
         assert np.array_equal(out[i], ref), f"frame {i}: {(out[i] != ref).sum()} px differ"
     m.close()
+
+
+def test_two_chain_paths_randomized(oracle):
+    """Random shapes and parameters where the two-chain kernels engage (> 1024 E/W chains, > 2048
+    3WAY column chains, D <= 128), adversarial pairs included (int16 extremes)."""
+    pytest.importorskip("hypothesis")
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    @settings(max_examples=6, deadline=None, derandomize=True, database=None,
+              suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+    @given(D=st.integers(1, 8).map(lambda k: 16 * k), H=st.integers(520, 640), W1=st.integers(520, 760),
+               mode=st.sampled_from([2, 3]), bs=st.sampled_from([3, 5, 7]), P1=st.integers(1, 600),
+               P2x=st.integers(2, 6), kind=st.sampled_from(["textured", "noise", "binary", "steps"]),
+               seed=st.integers(0, 10**6))
+    def run(D, H, W1, mode, bs, P1, P2x, kind, seed):
+        W = W1 + D
+        args = (0, D, bs, P1, P1 * P2x, 1, 63, 10, 0, 2, mode)
+        if kind == "textured":
+            L, R, _ = S.make_pair(H, W, D, seed=seed)
+        else:
+            L, R = S.adversarial_pair(kind, H, W, D, seed=seed)
+        dev = torch.device("cuda", 0)
+        m = sdr.StereoSGBM.create(*args)
+        out = m.compute(torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)).cpu().numpy()
+        ref = oracle.sgbm_compute(L, R, oracle.make_params(*args))
+        m.close()
+        assert np.array_equal(out, ref), f"{(out != ref).sum()} px differ"
+
+    run()

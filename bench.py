@@ -184,6 +184,30 @@ def load_traffic(kernel_tag):
         return None
 
 
+def stream_probe(dev, mib=2048, iters=10):
+    """This box's streaming rate: a device-to-device copy of a 2 GiB buffer (read + write bytes
+    over time), the ceiling a bandwidth-bound kernel of the same box can be held against --
+    the box-to-box spread of the HBM rate shows up here and in `roofline.achieved` alike."""
+    import torch
+
+    n = mib << 20
+    a_ = torch.empty(n, dtype=torch.uint8, device=dev)
+    b_ = torch.empty(n, dtype=torch.uint8, device=dev)
+    a_.fill_(1)
+    b_.copy_(a_)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        b_.copy_(a_)
+    e1.record()
+    torch.cuda.synchronize()
+    s_ = e0.elapsed_time(e1) / 1e3 / iters
+    del a_, b_
+    return {"gbs": round(2 * n / s_ / 1e9, 1), "what": f"torch device copy of {mib} MiB (read + write bytes), "
+                                                        f"mean of {iters} back to back"}
+
+
 def free_port() -> int:
     """A free TCP port on 127.0.0.1 for the ranks' rendezvous."""
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -237,9 +261,15 @@ def parse_args(argv=None):
                          "(roofline.in_flight; the events cost ~2 %% of the frame rate)")
     ap.add_argument("--streams", type=int, default=3, help="frames in flight (one matcher + stream each)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
+    ap.add_argument("--stream-probe", action=argparse.BooleanOptionalAction, default=True,
+                    help="time a 2 GiB device copy after the run (roofline.stream_probe: this box's "
+                         "streaming rate beside the dominant kernel's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses the N>1 path with every "
                          "rank on the one GPU of a 1-GPU box (gather staged through host memory)")
+    ap.add_argument("--dist-world1", action="store_true",
+                    help="run the distributed path (process group, gathers, gather_check) at world size 1 "
+                         "under torch.distributed.run --nproc-per-node 1 (RCCL on a one-GPU box)")
     ap.add_argument("--status-every", type=int, default=16,
                     help="N>1: ranks exchange their step status (host-side, gloo) every this many steps "
                          "and after the last; a failed rank keeps joining the gathers with zeros until "
@@ -261,6 +291,12 @@ def main():
         sys.exit(relay(launcher_cmd(a.gpus, free_port(), sys.argv[1:]), a.gpus,
                        env=dict(os.environ, SDR_BENCH_SELF_LAUNCHED="1")))
     world = int(env_world or "1")
+    # --dist-world1: the distributed data path (RCCL process group, status exchanges, the gather to
+    # rank 0 and its check) at world size 1, under torch.distributed.run --nproc-per-node 1, so the
+    # path the 8-GPU run takes executes on a one-GPU box too
+    dist_on = world > 1 or a.dist_world1
+    if a.dist_world1 and env_world is None:
+        raise SystemExit("bench: --dist-world1 runs under a launcher (torch.distributed.run --nproc-per-node 1)")
     if world != a.gpus:
         raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}: the launcher and the "
                          f"arguments disagree on the number of ranks")
@@ -273,7 +309,7 @@ def main():
     gloo = a.dist_backend == "gloo"
     from stereo_depth_ruler_amd.distributed import check_ranks, error_code, init_process_group
 
-    if world > 1:
+    if dist_on:
         # every collective bounded by SDR_DIST_TIMEOUT (default 120 s): a rank that dies outright
         # cannot leave the others blocked (stereo_depth_ruler_amd/distributed.py)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -306,6 +342,7 @@ def main():
                     "k_south_wta": _sg.KERNEL_WTA_LR, "k_lr_check": _sg.KERNEL_LR_CHECK,
                     "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
                     "reproject": _sg.KERNEL_REPROJECT, "k_sweep": _sg.KERNEL_SWEEP,
+                    "k_sweep_down": _sg.KERNEL_SWEEP_DOWN,
                     "k_wls_prep": _sg.KERNEL_WLS_PREP, "fgs_pass": _sg.KERNEL_FGS,
                     "k_wls_final": _sg.KERNEL_WLS_FINAL}
 
@@ -357,7 +394,7 @@ def main():
             return pipes[k].enqueue(sbs[j:j + batch], streams[k])
     m = ms[0]
     gather_bufs = None
-    if world > 1 and rank == 0:  # RCCL has no int16: gather the disparity bytes
+    if dist_on and rank == 0:  # RCCL has no int16: gather the disparity bytes
         gather_bufs = [[torch.empty(gather_bytes, dtype=torch.uint8, device="cpu" if gloo else dev)
                         for _ in range(world)]
                        for _ in range(2 * ns)]
@@ -382,15 +419,15 @@ def main():
                     raise SDRError(-1, f"injected failure at rank {rank} step {i}")
                 res = run(j, k, slot)
             except Exception as e:  # noqa: BLE001 -- any failed step is reported to every rank
-                if world == 1:
+                if not dist_on:
                     raise
                 if failure["err"] is None:
                     failure["code"], failure["err"] = error_code(e), e
                     log(f"rank {rank}: step {i} failed ({e!r}); reporting at the next status check")
                 res = torch.zeros((gather_bytes,), dtype=torch.uint8, device=dev)
-            if world > 1 and ((i + 1) % max(1, a.status_every) == 0):
+            if dist_on and ((i + 1) % max(1, a.status_every) == 0):
                 check_ranks(failure["code"])  # RankFailure on every rank if any step failed
-            if world > 1:
+            if dist_on:
                 # gather this step's disparity from every rank; a later step reuses the slot only
                 # after this collective has completed
                 src = as_bytes(res) if res.dtype != torch.uint8 else res
@@ -406,14 +443,14 @@ def main():
     for p in pending:
         if p is not None:
             p.wait()
-    if world > 1:
+    if dist_on:
         check_ranks(failure["code"])
     pending = [None] * (2 * ns)
     torch.cuda.synchronize()
     if not a.no_kernel_timing and a.in_flight_timing:
         m.enable_timing(2)
         m.kernel_time(-1, reset=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -423,13 +460,26 @@ def main():
         if p is not None:
             p.wait()
     torch.cuda.synchronize()
-    if world > 1:
+    # a batched MODE_HH step whose row sweep gave up waiting wrote INVALID frames and reports it
+    # here (sdr_sgbm_last_status): such a run has no valid number.  Every rank checks its own
+    # matchers before the last status exchange, so a rank that finds one fails every rank there
+    # instead of leaving the others in the collectives below
+    for mm in ms:
+        try:
+            mm.check_status()
+        except SDRError as e:
+            if not dist_on:
+                raise
+            if failure["err"] is None:
+                failure["code"], failure["err"] = error_code(e), e
+                log(f"rank {rank}: {e!r}")
+    if dist_on:
         check_ranks(failure["code"])
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ranks = None
-    if world > 1:
+    if dist_on:
         # every rank's own wall time (host-side exchange), then the max over ranks
         per_rank = [None] * world
         dist.all_gather_object(per_rank, {"rank": rank, "device": dev.index, "host": socket.gethostname(),
@@ -439,12 +489,8 @@ def main():
                  "launcher": ("bench.py --gpus (torch.distributed.run child)"
                               if os.environ.get("SDR_BENCH_SELF_LAUNCHED") else "external"),
                  "per_rank": per_rank}
-    # a batched MODE_HH step whose row sweep gave up waiting wrote INVALID frames and reports it
-    # here (sdr_sgbm_last_status): such a run has no valid number
-    for mm in ms:
-        mm.check_status()
     gather_check = None
-    if world > 1:
+    if dist_on:
         # end-to-end check of the data path (after the timed region): rank 0's copy of every rank's
         # bytes from the last timed step equals what that rank sent (position-weighted checksums)
         def cks(b):
@@ -467,37 +513,52 @@ def main():
     cells = nmatch * batch * Hm * w1 * D
     P = NPATHS[mode]
 
-    def kernel_report(mm, extra=None):
+    def kernel_report(mm, extra=None, step_us=None, steps=1):
         """Per-kernel HIP-event times of matcher mm since its last reset -> (kernels, roofline).
-        extra: {name: (total_ms, launches)} of launches timed outside the handle (the ingest)."""
+        extra: {name: (total_ms, launches)} of launches timed outside the handle (the ingest).
+        step_us: the single-stream step time of the same launches with no events (None: no
+        correction).  An event pair around a launch also spans its dispatch (~2 us a launch on
+        MI355X), so the events' sum exceeds the step; the excess per launch is subtracted from
+        every kernel's average (`avg_us`; the raw figure is `avg_us_events`), which puts the
+        per-kernel table in line with rocprofv3's kernel durations and its sum at or below the
+        step.  steps: the steps the events cover (per-step times)."""
         per_kind = {name: mm.kernel_time(kind, reset=False) for name, kind in KERNEL_KINDS.items()}
         all_ms, _ = mm.kernel_time(-1, reset=True)
         for name, v in (extra or {}).items():
             per_kind[name] = v
             all_ms += v[0]
-        kern = {name: {"avg_us": round(ms / c * 1e3, 2), "launches": c,
-                       "share": round(ms / all_ms, 4) if all_ms else None}
-                for name, (ms, c) in per_kind.items() if c}
-        frames_seen = per_kind["prefilter"][1]
+        launches = sum(c for _, c in per_kind.values())
+        ovh_us = 0.0
+        if step_us is not None and launches:
+            ovh_us = max(0.0, (all_ms * 1e3 - step_us * steps) / launches)
+        corr = {name: (ms - c * ovh_us / 1e3, c) for name, (ms, c) in per_kind.items()}
+        all_corr = sum(ms for ms, c in corr.values() if c)
+        kern = {name: {"avg_us": round(ms / c * 1e3, 2), "avg_us_events": round(per_kind[name][0] / c * 1e3, 2),
+                       "launches": c, "share": round(ms / all_corr, 4) if all_corr else None}
+                for name, (ms, c) in corr.items() if c}
         if not per_kind["k_paths"][1]:
             return kern, None
-        # algorithmic bytes per launch of the three path kernels (2 B per int16 cell):
+        # algorithmic bytes per launch of the path kernels (2 B per int16 cell):
         #   k_paths: each of its directions reads C and writes its own record;
-        #   k_sweep (batched MODE_HH): one pass reads C once and writes one record for its
-        #     directions (up: N, NE, NW; down: SE, SW), so k_paths keeps E and W only;
+        #   k_sweep (batched MODE_HH, up: N, NE, NW) and k_sweep_down (SE, SW): one pass reads C
+        #     once and writes one record for its directions, so k_paths keeps E and W only;
         #   k_south_wta: reads C and the other directions' records (top-to-bottom fused)
         sweep = per_kind["k_sweep"][1] > 0
         kp_dirs = 2 if sweep else P - 1
-        nrec = 4 if sweep else P - 1
+        nrec = 3 if sweep else P - 1
         models = {
             "k_paths": (cells * 4 * kp_dirs, f"4*{kp_dirs}*cells: {kp_dirs} directions "
-                        f"({'E, W; the others in k_sweep' if sweep else 'all but top-to-bottom'}), "
+                        f"({'E, W; the others in k_sweep16' if sweep else 'all but top-to-bottom'}), "
                         f"C read + record write each"),
-            "k_sweep": (cells * 4, "4*cells: one C read + one record write per pass (halo re-reads excluded)"),
+            "k_sweep": (cells * 4, "4*cells: one C read + one record write (up pass: N, NE, NW; halo re-reads "
+                        "excluded)"),
+            "k_sweep_down": (cells * 8, "8*cells: C + the E, W, up records read (down pass: S, SE, SW and the "
+                             "WTA; halo re-reads excluded)"),
             "k_south_wta": (cells * 2 * (1 + nrec), f"2*(1+{nrec})*cells: C + {nrec} records read"),
         }
-        name = max((n for n in models if per_kind[n][1]), key=lambda n: per_kind[n][0])
-        tot_ms, cnt = per_kind[name]
+        # the dominant kernel: the largest per-step time of ONE kernel (each kind is one kernel)
+        name = max((n for n in models if per_kind[n][1]), key=lambda n: corr[n][0])
+        tot_ms, cnt = corr[name]
         bytes_per_launch, model = models[name]
         avg_s = tot_ms / cnt / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
@@ -505,7 +566,8 @@ def main():
             "k_paths": f"k_paths<DPL={2 if D <= 128 else 4}> or k_paths_tc (two chains per wave, the engine's pick "
                        f"for latency-bound launches) ({kp_dirs} of the {P} path directions of a batch in "
                        f"one launch; the top-to-bottom one is fused into k_south_wta)",
-            "k_sweep": "k_sweep (row-synchronous up/down passes of batched MODE_HH)",
+            "k_sweep": "k_sweep16 up pass (row-synchronous N, NE, NW of batched MODE_HH)",
+            "k_sweep_down": "k_sweep16 down pass (row-synchronous S, SE, SW of batched MODE_HH + the WTA)",
             "k_south_wta": f"k_south_wta (top-to-bottom path fused with the WTA, reading {nrec} records)",
         }[name]
         roof = {
@@ -519,16 +581,26 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "bytes_model": f"{model}; cells={'2 matchers*' if nmatch == 2 else ''}batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),
+            "avg_launch_us_events": round(per_kind[name][0] / cnt * 1e3, 2),
+            "event_overhead_us_per_launch": round(ovh_us, 2),
             "launches_timed": cnt,
-            "kernel_share_of_gpu_time": round(tot_ms / all_ms, 4) if all_ms else None,
+            "kernel_share_of_gpu_time": round(tot_ms / all_corr, 4) if all_corr else None,
         }
+        # the other path kernels at their own rates (each against its own byte model)
+        roof["path_kernels"] = {
+            n: {"avg_us": round(corr[n][0] / corr[n][1] * 1e3, 2),
+                "achieved": round(models[n][0] / (corr[n][0] / corr[n][1] / 1e3) / 1e9, 1),
+                "frac": round(models[n][0] / (corr[n][0] / corr[n][1] / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+            for n in models if per_kind[n][1]}
         # whole pipeline: cost write + the path kernels' data flow above, over the summed kernel
         # time of one step
-        pipe_bytes = cells * (2 + 4 * kp_dirs + (8 if sweep else 0) + 2 * (1 + nrec))
-        gpu_s = all_ms / 1e3 / max(1, frames_seen)
+        # (batched MODE_HH: cost 2 + E/W 8 + up 4 + down with the WTA 8 = 22 B a cell)
+        pipe_bytes = cells * (2 + 4 * kp_dirs + (4 + 8 if sweep else 2 * (1 + nrec)))
+        gpu_s = all_corr / 1e3 / max(1, steps)
         roof["pipeline"] = {
             "algorithmic_bytes_per_step": pipe_bytes,
             "kernel_time_per_step_us": round(gpu_s * 1e6, 1),
+            "single_stream_step_us": round(step_us, 1) if step_us is not None else None,
             "achieved": round(pipe_bytes / gpu_s / 1e9, 1),
             "frac": round(pipe_bytes / gpu_s / 1e9 / HBM_PEAK_GBS, 4),
         }
@@ -539,7 +611,7 @@ def main():
     if not a.no_kernel_timing:
         inflight = None
         if a.in_flight_timing:
-            _, inflight = kernel_report(m)
+            _, inflight = kernel_report(m, steps=a.steps)
             if inflight is not None:
                 inflight["measured"] = (f"HIP events around each launch of matcher 0 over the timed region "
                                         f"({ns} frames in flight: an event pair also spans the wait for CUs "
@@ -548,28 +620,46 @@ def main():
         # single-stream segment timed right after the timed region (no events inside the timed
         # region; rocprofv3's per-dispatch durations of these launches agree:
         # profiles/r2_segments_c2.md)
+        iso = max(1, a.iso_steps)
+
+        def iso_run(timed):
+            ingest = []
+            with torch.cuda.stream(streams[0]):
+                for i in range(iso):
+                    j = (i * batch) % (nf - batch + 1) if nf > batch else 0
+                    if kind == "live" and timed:  # k_sbs_ingest runs on the rectifier's handle: torch events
+                        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                        ingest.append(ev)
+                        run(j, 0, 0, ingest_events=ev)
+                    else:
+                        run(j, 0, 0)
+            return ingest
+
+        # the same single-stream steps without events first: the step time the per-kernel table
+        # is reconciled with (kernel_report's step_us)
         torch.cuda.synchronize()
+        iso_run(False)  # warm
+        torch.cuda.synchronize()
+        t_iso = time.perf_counter()
+        iso_run(False)
+        torch.cuda.synchronize()
+        step_us = (time.perf_counter() - t_iso) / iso * 1e6
         m.enable_timing(2)
         m.kernel_time(-1, reset=True)
-        ingest = []
-        with torch.cuda.stream(streams[0]):
-            for i in range(max(1, a.iso_steps)):
-                j = (i * batch) % (nf - batch + 1) if nf > batch else 0
-                if kind == "live":  # k_sbs_ingest runs on the rectifier's handle: torch events
-                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                    ingest.append(ev)
-                    run(j, 0, 0, ingest_events=ev)
-                else:
-                    run(j, 0, 0)
+        ingest = iso_run(True)
         torch.cuda.synchronize()
         extra = {"k_sbs_ingest": (sum(e0.elapsed_time(e1) for e0, e1 in ingest), len(ingest))} if ingest else None
-        kernels, roofline = kernel_report(m, extra)
+        kernels, roofline = kernel_report(m, extra, step_us=step_us, steps=iso)
         if roofline is not None:
-            roofline["measured"] = (f"HIP events around each launch, {max(1, a.iso_steps)} single-stream steps "
-                                    f"after the timed region")
+            roofline["measured"] = (f"HIP events around each launch, {iso} single-stream steps after the timed "
+                                    f"region, less the events' own overhead per launch (the events' sum over "
+                                    f"the same {iso} steps run without events)")
             roofline["kernels"] = kernels
             if inflight is not None:
                 roofline["in_flight"] = inflight
+            if a.stream_probe:
+                roofline["stream_probe"] = stream_probe(dev)
+                roofline["frac_of_probe"] = round(roofline["achieved"] / roofline["stream_probe"]["gbs"], 4)
         m.enable_timing(0)
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6
@@ -603,7 +693,7 @@ def main():
                                 "disp12MaxDiff", "preFilterCap", "uniquenessRatio",
                                 "speckleWindowSize", "speckleRange", "mode"], args)),
             "parallelism": f"frame shard x{world}" + ((" + gloo gather to rank 0 (rehearsal)" if gloo else
-                                                      " + RCCL gather to rank 0") if world > 1 else ""),
+                                                      " + RCCL gather to rank 0") if dist_on else ""),
             "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),
@@ -622,7 +712,7 @@ def main():
         print(json.dumps(out), flush=True)
     for mm in closers:
         mm.close()
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

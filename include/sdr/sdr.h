@@ -86,8 +86,14 @@ int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p);
 int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p);
 /* HIP stream (hipStream_t) the handle launches on (NULL = the HIP null stream, e.g. torch's
  * default stream); a new handle uses a stream of its own, restored by sdr_sgbm_reset_stream.
- * Changing the stream orders the handle's pending work on the previous stream before the new
- * stream's (an event recorded there at the switch), so the previous stream must still exist. */
+ * Changing the stream orders the handle's earlier work before the new stream's: an event is
+ * recorded on the previous stream at the switch (not after every call: a record is a queue
+ * barrier, ~6 us of idle queue per class-path frame).  So a caller's stream must outlive the
+ * handle's use of it: move the handle off a stream (set another, or sdr_sgbm_reset_stream) before
+ * destroying that stream, and destroy the handle while its current stream exists.  HIP does not
+ * validate a destroyed stream's handle -- an event recorded on one, or waited on after it was
+ * recorded there, crashes the process (MI355X, ROCm 7.2, round 5) -- so the engine cannot detect
+ * a violation; tests/test_gpu_streams.py exercises the supported order. */
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
 int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);
@@ -381,11 +387,12 @@ enum {
     SDR_KERNEL_WTA_LR = 3,   /* k_south_wta: top-to-bottom path fused with WTA/uniqueness/disp2 */
     SDR_KERNEL_MEDIAN = 4, SDR_KERNEL_SPECKLE = 5, SDR_KERNEL_REPROJECT = 6,
     SDR_KERNEL_LR_CHECK = 7, /* the LR-checked map materialised (debug stage 2 only since round 3) */
-    SDR_KERNEL_SWEEP = 8,    /* k_sweep: batched MODE_HH's up (N, NE, NW) and down (SE, SW) passes */
+    SDR_KERNEL_SWEEP = 8,    /* k_sweep: batched MODE_HH's up pass (N, NE, NW) */
     /* the class path's WLS filter (sdr_stereo_class_*), recorded on the left matcher's handle */
     SDR_KERNEL_WLS_PREP = 9, /* k_wls_prep (or k_wls_disc + k_wls_conf past 4096 ROI columns) */
     SDR_KERNEL_FGS = 10,     /* one FGS pass: k_fgs_pcr, or k_fgs_sweep (+ its transposes) */
-    SDR_KERNEL_WLS_FINAL = 11 /* k_wls_final (+ /16 + computeDepth epilogue) */
+    SDR_KERNEL_WLS_FINAL = 11, /* k_wls_final (+ /16 + computeDepth epilogue) */
+    SDR_KERNEL_SWEEP_DOWN = 12 /* batched MODE_HH's down pass (SE, SW): timed apart from the up pass */
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);

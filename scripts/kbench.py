@@ -28,9 +28,10 @@ CONFIGS = {  # W, H, D, mode, frames
     "c4": (640, 360, 80, 2, 2),  # the class path's two matchers as two frames (1440 E/W chains)
     "c5b8": (1920, 1080, 256, 1, 8),  # C5 as benched: 8 frames through the row sweeps
     "hh128": (1280, 720, 128, 1, 8),  # the sweeps at two disparities per lane
+    "c3b32": (1280, 720, 256, 1, 32),  # C3 as benched: 32 frames per call
 }
 KINDS = ["prefilter", "k_cost", "k_paths", "k_south_wta", "median", "speckle", "reproject", "k_lr_check",
-         "k_sweep"]  # SDR_KERNEL_* order
+         "k_sweep", "k_wls_prep", "fgs_pass", "k_wls_final", "k_sweep_down"]  # SDR_KERNEL_* order
 
 
 def load(path):

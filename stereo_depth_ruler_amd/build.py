@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libsdr.so")
-SOURCES = ["sdr_cost.hip", "sdr_cost3.hip", "sdr_cost3k2.hip", "sdr_cost_generic.hip", "sdr_paths.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_rectify.hip",
+SOURCES = ["sdr_cost.hip", "sdr_cost3.hip", "sdr_cost3k2.hip", "sdr_cost_generic.hip", "sdr_paths.hip", "sdr_sweep.hip", "sdr_post.hip", "sdr_wls.hip", "sdr_rectify.hip",
            "sdr_cloud.hip", "sdr_display.hip", "sdr_engine.hip"]
 HEADERS = ["sdr_device.hpp", "sdr_internal.hpp", "sdr_cost_kernel.hpp"]
 ARCH = os.environ.get("SDR_OFFLOAD_ARCH", "gfx950")
@@ -79,6 +79,9 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
     if not variant and not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    # the build id is the hash of the sources as they are when the compile starts; if any of them
+    # changes before the link is done, the library is not a build of either version: fail
+    bid = source_hash()
     objdir = os.path.join(os.path.dirname(OUT), "obj" + (f"-{variant}" if variant else ""))
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
@@ -93,8 +96,10 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
         # an object is reused when its recorded hash (source, headers, flags) still matches
         key = _hash([os.path.join(CSRC, f)] + hdrs, flags)
         stamp = obj + ".hash"
-        if not force and os.path.exists(obj) and os.path.exists(stamp) and open(stamp).read() == key:
-            continue
+        if not force and os.path.exists(obj) and os.path.exists(stamp):
+            with open(stamp) as fh:
+                if fh.read() == key:
+                    continue
         cmd = [hipcc, *flags, "-c", os.path.join(CSRC, f), "-o", obj]
         if verbose:
             print(" ".join(cmd))
@@ -109,7 +114,7 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
     bid_src = os.path.join(objdir, "sdr_build_id.cpp")
     with open(bid_src, "w") as fh:
         fh.write('extern "C" const char* sdr_build_id(void) {\n'
-                 f'    static const char id[] = "SDR_BUILD_ID={source_hash()}";\n'
+                 f'    static const char id[] = "SDR_BUILD_ID={bid}";\n'
                  '    return id + 13;\n}\n')
     bid_obj = os.path.join(objdir, "sdr_build_id.o")
     subprocess.check_call([hipcc, "-O2", "-fPIC", "-x", "c++", "-c", bid_src, "-o", bid_obj])
@@ -118,6 +123,9 @@ def build_native(force: bool = False, verbose: bool = False, variant: str = "",
     if verbose:
         print(" ".join(link))
     subprocess.check_call(link)
+    if source_hash() != bid:
+        os.remove(out + ".tmp")
+        raise RuntimeError("the engine's sources changed during the build: run it again")
     os.replace(out + ".tmp", out)
     return out
 

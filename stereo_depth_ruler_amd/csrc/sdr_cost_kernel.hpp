@@ -365,16 +365,15 @@ static void launch_cost_t(const Geometry& g, CostArgs a, int F, hipStream_t st) 
     if (a.TY <= 0) {
         // one full pass of resident blocks: a partial second pass doubles the kernel time, and
         // each block re-walks NR-1 warm-up rows, so use the tallest row band that fills the chip
+        // blocks per CU: a property of the kernel and its LDS (one gfx950 binary), cached per LDS size
         static thread_local size_t key = 0;
-        static thread_local int slots = 0;
+        static thread_local int per_cu = 0;
         if (key != lds) {
-            int dev = 0, cus = 0, per_cu = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            per_cu = 0;
             (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_cost<NR, K, CN>, Cfg::NT, lds);
-            slots = max(1, cus * max(1, per_cu));
             key = lds;
         }
+        const int slots = max(1, device_cus() * max(1, per_cu));
         // the 3WAY stripe-start bands are extra rows of blocks in the same launch: leave them
         // their slots, or the launch spills into a second pass (C4: 828 blocks on 768 slots,
         // 61 -> 35 us)

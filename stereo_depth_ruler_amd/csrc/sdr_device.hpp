@@ -197,6 +197,21 @@ __device__ __forceinline__ void store_buf_nt(Rsrc r, uint32_t vofs, uint32_t sof
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
 
+// CUs of the current device (host side), cached per device id: a thread may drive handles on
+// several devices, so a per-thread cache of the first device's count would be wrong on another
+inline int device_cus() {
+    static int cache[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    int cus = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+    if (cus <= 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        __atomic_store_n(&cache[dev], cus, __ATOMIC_RELAXED);
+    }
+    return cus;
+}
+
 // Dispatch-order block index h (of n) -> logical index such that consecutive logical blocks share
 // an XCD (and its L2): blocks are dealt round-robin over the 8 XCDs, so h and h + 8 share one
 // (MI355X_MICROARCH.md, workgroup dispatch); the XCD of h % 8 gets a contiguous logical range.

@@ -345,7 +345,7 @@ struct sdr_sgbm {
     // recorded after the last kernel that touches this handle's scratch; a stream switch makes
     // the new stream wait for it, so one matcher used from two streams never overlaps itself
     hipEvent_t done = nullptr;
-    bool pending = false;
+    bool pending = false;  // work enqueued since the last switch, not yet recorded
     // the last compute skipped the no-op LR check (disp12MaxDiff >= D): debug stage 2 is then
     // rebuilt on request from the WTA map with this geometry
     bool lr_skipped = false;
@@ -368,24 +368,35 @@ bool capturing(hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
-// The handle's last enqueue, for the next stream that uses its scratch.  Recorded lazily: only
-// when the handle moves to another stream does its old stream get the event (after everything
-// queued there so far, the handle's work included), and the new stream wait on it.  An event
-// record is a queue barrier: recorded after every call it left a ~5.4 us idle gap per class-path
-// frame.  Hence the previous stream must still exist when the handle changes streams (as it must
-// for sdr_sgbm_destroy's synchronisation).  Nothing is recorded into or waited on from a graph
-// capture: the capture's replays order themselves.
-void retire(sdr_sgbm* h) { h->pending = true; }
+// The handle's last enqueue, for the next stream that uses its scratch (h->done).  Recorded lazily:
+// only when the handle moves to another stream does its old stream get the event (after everything
+// queued there so far, the handle's work included), and the new stream wait on it.  An event record
+// is a queue barrier: recorded after every call it left a ~6 us idle gap per class-path frame
+// (rounds 4 and 5).  Hence the previous stream must still exist when the handle changes streams,
+// as it must for sdr_sgbm_destroy's synchronisation (sdr.h: HIP does not validate a destroyed
+// stream, so this is the caller's contract, as for any library handle bound to a stream).  Nothing
+// is recorded into or waited on from a graph capture: the capture's replays order themselves.
+hipError_t retire(sdr_sgbm* h) {
+    h->pending = true;
+    return hipSuccess;
+}
 int use_stream(sdr_sgbm* h, hipStream_t s) {
     // a stream being captured neither queries nor waits on an event recorded outside the capture
     // (both invalidate a global-mode capture); torch.cuda.graph synchronises before it captures,
     // and a caller capturing by hand orders the handle's earlier work before the capture itself
-    if (s != h->stream && h->pending && h->done && !capturing(h->stream) && !capturing(s)) {
-        SDR_HIP(hipEventRecord(h->done, h->stream));
-        SDR_HIP(hipStreamWaitEvent(s, h->done, 0));
+    if (s == h->stream) return SDR_OK;
+    hipError_t e = hipSuccess;
+    if (h->pending && h->done && !capturing(h->stream) && !capturing(s)) {
+        e = hipEventRecord(h->done, h->stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, h->done, 0);
     }
-    if (s != h->stream) h->pending = false;
+    // the handle moves to s even when the ordering failed: the error is reported once and the
+    // handle stays usable on s
+    h->pending = false;
     h->stream = s;
+    if (e != hipSuccess)
+        return fail(SDR_ERR_DEVICE, std::string("ordering the handle's previous stream before the new one: ") +
+                                        hipGetErrorString(e));
     return SDR_OK;
 }
 }  // namespace
@@ -473,6 +484,16 @@ static bool can_pair(const Eff& a, const Eff& b) {
 static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int W, int H,
                            size_t stride, size_t fstride, int F, int16_t* out, int* out_min,
                            int16_t** final_disp, int cn = 1, const sdr_sgbm_params* pair = nullptr) {
+    // a batch of an earlier call whose sweep wait gave up (its frames were written as INVALID):
+    // reported here, by the next call, if no sdr_sgbm_last_status has reported it yet.  The
+    // host copy is refreshed asynchronously after every sweep batch, so this check never waits
+    // (a timeout still in flight is reported by the call after)
+    if (h->status_host && __atomic_load_n(h->status_host, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(h->status_host, 0, __ATOMIC_RELEASE);
+        SDR_HIP(hipMemsetAsync(h->status.p, 0, sizeof(int), h->stream));
+        return fail(SDR_ERR_DEVICE, "an earlier MODE_HH batch's row sweep timed out waiting for a neighbouring "
+                                    "tile: that batch's frames were written as INVALID (this call did not run)");
+    }
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
@@ -502,16 +523,16 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
 
     const size_t cells = (size_t)H * g.W1 * g.D;
     const int P = npaths_of(e.mode);
-    // batched MODE_HH: N/NE/NW and SE/SW as two row-synchronous sweeps into one record each
-    // (when every tile of the frames in flight fits the resident grid); the records are then
-    // E, W, up, down -- saturated sums of non-negative path costs, so the grouping is exact
-    sdr::SweepShape shp[2] = {};  // [0]: down (SE, SW), [1]: up (N, NE, NW)
+    // batched MODE_HH: N/NE/NW and S/SE/SW as two row-synchronous sweeps (when every tile of the
+    // frames in flight fits the resident grid); the records are then E, W and up -- saturated sums
+    // of non-negative path costs, so the grouping is exact -- and the down sweep runs the WTA
+    sdr::SweepShape shp[2] = {};  // [0]: down (S, SE, SW + WTA), [1]: up (N, NE, NW)
     // (not inside a graph capture: its replays could overlap another sweep's, which the event
     // chain below orders for directly enqueued sweeps only)
     if (e.mode == SDR_MODE_HH && F >= kSweepMinFrames && g.W1 > 0 && !capturing(h->stream))
         for (int up = 0; up < 2; up++) shp[up] = sdr::sweep_shape(g, F, up != 0);
     const bool sweep = shp[0].nslots > 0 && shp[1].nslots > 0;
-    const int nrec = sweep ? 4 : P - 1;  // L records per pixel
+    const int nrec = sweep ? 3 : P - 1;  // L records per pixel
     std::vector<Stripe> stripes;
     if (e.mode == SDR_MODE_SGBM_3WAY) stripes_of(e, &stripes);
     if (stripes.size() + 2 > (size_t)sdr::kMaxPathDirs) return fail(SDR_ERR_ARG, "too many 3WAY stripes");
@@ -552,8 +573,8 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     // [pass][slots][tiles][2] counters, the error word, then the edge ring (sized for either pass)
     size_t flags_n[2] = {0, 0}, edge_bytes = 0;
     for (int up = 0; up < 2; up++) {
-        flags_n[up] = (size_t)shp[up].nslots * shp[up].ntiles * 2;
-        edge_bytes = std::max(edge_bytes, (size_t)shp[up].nslots * shp[up].ntiles * 4 * shp[up].cols * g.D * 2);
+        flags_n[up] = (size_t)shp[up].nslots * shp[up].ntiles * 2 * shp[up].npub;
+        edge_bytes = std::max(edge_bytes, (size_t)shp[up].nslots * shp[up].ntiles * 4 * shp[up].entry_words * 4);
     }
     const size_t sweep_flags = (flags_n[0] + flags_n[1]) * sizeof(int);
     if (sweep) {
@@ -668,7 +689,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         add_dir(plS, sdr::DIR_S, nS, nullptr);
         add_dir(pls, sdr::DIR_N, nS, buf());
     } else if (sweep) {
-        add_dir(plS, sdr::DIR_S, nS, nullptr);  // records 2 and 3: the up and down sweeps
+        // record 2: the up sweep; S, SE and SW run in the down sweep with the WTA
     } else {
         add_dir(plS, sdr::DIR_S, nS, nullptr);
         if (e.mode == SDR_MODE_HH) add_dir(pls, sdr::DIR_N, nS, buf());
@@ -707,6 +728,13 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         sa.err = (int*)(sb + sweep_flags);
         sa.edge = (uint32_t*)(sb + sweep_flags + 256);
         sa.spin = h->sweep_spin;
+        sdr::SweepWta sw{};
+        sw.recs = Lr;
+        sw.disp_raw = draw;
+        sw.d2 = d2;
+        sw.disp_fstride = px;
+        sw.uniq = e.uniq;
+        sw.uniq_simd = e.uniq_simd;
         std::lock_guard<std::mutex> lk(g_sweep_mu);
         hipEvent_t& last = g_sweep_last[h->device];
         if (last) SDR_HIP(hipStreamWaitEvent(st, last, 0));
@@ -715,24 +743,27 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
             sa.up = up;
             sa.ntiles = shp[up].ntiles;
             sa.nslots = shp[up].nslots;
-            sa.rec = Lr + (size_t)(up ? 2 : 3) * g.D;
-            KTimer kt(h, SDR_KERNEL_SWEEP);
-            sdr::launch_sweep(g, sa, F, st);
+            sa.rec = Lr + (size_t)2 * g.D;
+            KTimer kt(h, up ? SDR_KERNEL_SWEEP : SDR_KERNEL_SWEEP_DOWN);
+            sdr::launch_sweep(g, sa, sw, F, st);
             sa.flags += flags_n[up];
         }
         SDR_HIP(hipEventRecord(last, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[2], st));
 
-    sdr::SouthWtaArgs wa{};
-    wa.L = Lr;
-    wa.npaths = nrec + 1;
-    wa.disp_raw = draw;
-    wa.d2 = d2;
-    wa.disp_fstride = px;
-    wa.uniq = e.uniq;
-    wa.uniq_simd = e.uniq_simd;
-    { KTimer kt(h, SDR_KERNEL_WTA_LR); sdr::launch_south_wta(g, plS, wa, F, st); }
+    if (!sweep) {
+        sdr::SouthWtaArgs wa{};
+        wa.L = Lr;
+        wa.npaths = nrec + 1;
+        wa.disp_raw = draw;
+        wa.d2 = d2;
+        wa.disp_fstride = px;
+        wa.uniq = e.uniq;
+        wa.uniq_simd = e.uniq_simd;
+        KTimer kt(h, SDR_KERNEL_WTA_LR);
+        sdr::launch_south_wta(g, plS, wa, F, st);
+    }
     const sdr::LrSrc lr{g, draw, d2, px, e.disp12MaxDiff};
     if (speckle) {
         // the LR check and the median filter run inside the labelling's first pass (dfin = median
@@ -759,7 +790,7 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
         SDR_HIP(hipMemcpyAsync(h->status_host, h->status.p, sizeof(int), hipMemcpyDeviceToHost, st));
     }
     if (h->timing) SDR_HIP(hipEventRecord(h->ev[3], st));
-    retire(h);
+    SDR_HIP(retire(h));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -825,6 +856,7 @@ int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
     if (h->status_host) (void)hipHostFree(h->status_host);
     for (Buf* b : {&h->sweep, &h->status, &h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
                    &h->labels, &h->sizes, &h->mins, &h->hin, &h->hxyz, &h->cls_bgr,
@@ -947,7 +979,7 @@ int sdr_sgbm_compute_device_cn(sdr_sgbm* h, const uint8_t* dL, const uint8_t* dR
         for (int f = 0; f < F; f++)
             SDR_HIP(hipMemcpy2DAsync(dDisp + f * disp_fstride, disp_stride * 2, fin + f * px, W * 2,
                                      W * 2, H, hipMemcpyDeviceToDevice, h->stream));
-        retire(h);
+        SDR_HIP(retire(h));
     }
     return SDR_OK;
 }
@@ -970,7 +1002,7 @@ int sdr_sgbm_compute_reproject_device(sdr_sgbm* h, const uint8_t* dL, const uint
         sdr::launch_reproject_s16(fin, W, H, W, px, Q, handle_missing, mins, dXYZ, (size_t)W * 3,
                                   px * 3, F, h->stream);
     }
-    retire(h);
+    SDR_HIP(retire(h));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -1036,7 +1068,7 @@ int sdr_sgbm_compute_reproject(sdr_sgbm* h, const uint8_t* left, const uint8_t* 
                                   h->stream);
     }
     SDR_HIP(hipGetLastError());
-    retire(h);
+    SDR_HIP(retire(h));
     if ((rc = h->hx.download(xyz, xyz_stride * 4, dX, (size_t)W * 12, (size_t)W * 12, H, h->stream))) return rc;
     return h->hx.drain();
 }
@@ -1248,9 +1280,10 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         hipStream_t rs = right->stream;
         if ((rc = use_stream(right, left->side))) return rc;
         rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
-        retire(right);
+        const hipError_t re = retire(right);
         const int rc2 = use_stream(right, rs);
         if (rc) return rc;
+        SDR_HIP(re);
         if (rc2) return rc2;
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
@@ -1272,7 +1305,7 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         if (d_xyz)
             sdr::launch_reproject_f32(d_out, w2, h2, w2, px2, Q, 0, nullptr, d_xyz, (size_t)w2 * 3, px2 * 3, F, st);
     }
-    retire(left);
+    SDR_HIP(retire(left));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }

@@ -135,31 +135,33 @@ struct PathLaunch {
     RowRedirect redir[kMaxCostAux];
 };
 
-// Row-synchronous sweeps of batched MODE_HH (sdr_paths.hip, k_sweep): the upward directions N, NE
-// and NW (up = 1) or the downward diagonals SE and SW (up = 0) of a frame in one pass over its
-// rows, column tiles of kSweepTile columns per workgroup handing the diagonals' tile-edge path
-// costs to their neighbours each row.  Each pass reads a cost row once for all its directions
-// and writes their saturated sum as one record slot.
+// Row-synchronous sweeps of batched MODE_HH (sdr_sweep.hip, k_sweep16): the upward directions N,
+// NE and NW (up = 1) into one record, or the downward S, SE and SW (up = 0) summed with the E, W
+// and up records into S and reduced by the WTA (A.8) in the same step.  A workgroup walks a column
+// tile of a frame row by row, one pixel per 16-lane row of a wave; halo waves recompute the
+// diagonals' tile-edge columns and reload them from the neighbour tiles through a global ring.
 constexpr int kSweepOwn = 10;                     // waves holding the tile's own columns
 constexpr int kSweepWaves = kSweepOwn + 2;        // + one halo wave on each side
-// columns per wave: 8, or 6 for the three-direction pass at D > 128 (its 48 path-cost words per
-// lane and column must fit 3 waves per SIMD without spilling); tile = kSweepOwn waves of them.
-// A halo reload every cols - 1 rows: a halo column j (counted from the tile's far side) goes wrong
-// j rows after a reload, and the tile's first column takes the halo's nearest one from the row
-// before through LDS, which the halo wave computed before the reload
-__host__ __device__ constexpr int sweep_cols(int dpl, bool up) { return dpl == 4 && up ? 6 : 8; }
 struct SweepArgs {
     const int16_t* C;
     size_t cs_fstride;     // elements per frame of C
-    int16_t* rec;          // this pass's record slot (L records + slot * D)
+    int16_t* rec;          // up pass: its record slot (L records + slot * D)
     size_t l_fstride;      // elements per frame of the records
     int l_pix;             // elements per pixel record
-    uint32_t* edge;        // [nslots][ntiles][2 sides][2][cols][D/2] boundary columns' path costs
-    int* flags;            // [nslots][ntiles][2 sides] rows published (zero before the launch)
+    uint32_t* edge;        // [nslots][ntiles][2 sides][2 parities][entry_words] the tile edges' path costs
+    int* flags;            // [nslots][ntiles][2 sides][npub] rows published (zero before the launch)
     int* err;              // set when a neighbour wait times out (never, with every tile resident)
     int ntiles, nslots;    // frames in flight = nslots (workgroups = nslots * ntiles, all resident)
     int up;
     int spin;              // polls before a wait gives up (kSweepSpin; lower through a debug knob)
+};
+// the down pass's WTA (A.8): the E, W, up records it reads and the outputs k_south_wta would write
+struct SweepWta {
+    const int16_t* recs;   // [F][H][W1][3][D]: E, W, up
+    int16_t* disp_raw;     // [F][H][W] WTA disparity (matched columns only)
+    uint32_t* d2;          // [F][H][W] right-view WTA keys (SouthWtaArgs::d2), nullable
+    size_t disp_fstride;
+    int uniq, uniq_simd;
 };
 constexpr int kSweepSpin = 1 << 20;  // polls (~1 us each) before a sweep's wait gives up
 // After a batch's sweeps and post-filter: when a wait of this call's sweeps timed out (*err), the
@@ -168,13 +170,13 @@ constexpr int kSweepSpin = 1 << 20;  // polls (~1 us each) before a sweep's wait
 // (sdr_sgbm_last_status reports it).  Nothing happens otherwise.
 void launch_sweep_verdict(const int* err, int16_t* disp, size_t n, int F, int16_t invalid, int* mins,
                           int* sticky, hipStream_t st);
-// a pass's tiling: columns per wave, tiles per frame, frames in flight (slots; 0: the frame's
-// tiles do not fit the resident grid)
+// a pass's tiling: own columns per wave, tiles per frame, frames in flight (slots; 0: the frame's
+// tiles do not fit the resident grid), publishing waves per tile edge, words of one ring entry
 struct SweepShape {
-    int cols, ntiles, nslots;
+    int cols, ntiles, nslots, npub, entry_words;
 };
 SweepShape sweep_shape(const Geometry& g, int F, bool up);
-void launch_sweep(const Geometry& g, const SweepArgs& a, int F, hipStream_t st);
+void launch_sweep(const Geometry& g, const SweepArgs& a, const SweepWta& w, int F, hipStream_t st);
 
 // top-to-bottom direction fused with the WTA (sdr_paths.hip): the other P-1 directions' L in
 // sum order with the fused direction at position kSouthIdx

@@ -86,9 +86,8 @@ __device__ __forceinline__ void step_words(const Regs<K>& c, const Regs<K>& Lp, 
 // the lane without a source (lane 0 / lane 63) unwritten, so passing the previous shift as the
 // DPP's old value keeps the kMaxPair boundary there from the first step on, with no refill.
 // (An offset-carrying form that takes the wave minimum off the serial chain was bit-exact and
-// not faster on MI355X)
-// UNIFORM: the wave minimum as a scalar (k_paths: one chain per wave); false: broadcast in a VGPR
-template <int K, bool PAD, bool UNIFORM = true>
+// not faster on MI355X)  The wave minimum is a wave-uniform (SGPR) value.
+template <int K, bool PAD>
 __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& delta2, uint32_t P1x2,
                                              uint32_t P2x2, bool active, uint32_t& upr, uint32_t& dnr) {
     if constexpr (PAD) {
@@ -104,58 +103,9 @@ __device__ __forceinline__ Regs<K> path_step(Regs<K> c, Regs<K>& Lp, uint32_t& d
     // wave minimum as a wave-uniform value, splatted and offset by P2 in scalar registers
     const uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu),
                                                               (unsigned short)(m >> 16));
-    delta2 = (UNIFORM ? wave_min_u32_uniform(m16) : wave_min_u32(m16)) * 0x00010001u + P2x2;
+    delta2 = wave_min_u32_uniform(m16) * 0x00010001u + P2x2;
     Lp = L;
     return L;
-}
-
-// The recurrence of one step without its wave minimum: returns L and leaves the lane's minimum
-// over its pairs (low half) in m16, for callers that reduce several chains' minima together
-// (k_sweep, wave_deltas: interleaved, so the DPP steps' wait states overlap).
-template <int K, bool PAD>
-__device__ __forceinline__ Regs<K> path_step_min16(Regs<K> c, const Regs<K>& Lp, uint32_t delta2, uint32_t P1x2,
-                                                   bool active, uint32_t& upr, uint32_t& dnr, uint32_t& m16) {
-    if constexpr (PAD) {
-#pragma unroll
-        for (int i = 0; i < K; i++) c.r[i] = active ? c.r[i] : kMaxPair;
-    }
-    const uint32_t up = upr = lane_from_prev(Lp.r[K - 1], upr);
-    const uint32_t dn = dnr = lane_from_next(Lp.r[0], dnr);
-    Regs<K> L;
-    uint32_t m;
-    step_words<K, PAD>(c, Lp, delta2, P1x2, active, up, dn, L, m);
-    m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu), (unsigned short)(m >> 16));
-    return L;
-}
-
-// N wave-uniform minima (wave_min_u32_uniform's steps) reduced together, step by step: each DPP
-// step of one value is N-1 instructions after the previous one, past the 2-wait-state VALU ->
-// DPP read hazard that a single reduction pays as an s_nop per step.  Returns min * 0x10001 + P2.
-template <int N>
-__device__ __forceinline__ void wave_deltas(uint32_t (&m)[N], uint32_t (&delta2)[N], uint32_t P2x2) {
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppQuadXor1>(m[i]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppQuadXor2>(m[i]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppRowHalfMirror>(m[i]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) m[i] = min_u32_dpp<kDppRowMirror>(m[i]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++)
-        m[i] = min(m[i], (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m[i], 0x142, 0xa, 0xf, false));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++)
-        m[i] = min(m[i], (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)m[i], 0x143, 0xc, 0xf, false));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < N; i++) delta2[i] = (uint32_t)__builtin_amdgcn_readlane((int)m[i], 63) * 0x00010001u + P2x2;
 }
 
 // k_paths lookahead (steps).  32 steps at D <= 128 measured slower on the class path's 640x360
@@ -406,14 +356,7 @@ static bool paths_two_chain(const Geometry& g, const PathLaunch& pl, int F) {
     if (g.D > 128 || pl.nredir > 0) return false;
     for (int i = 0; i < pl.ndirs; i++)
         if (pl.d[i].dir != DIR_E && pl.d[i].dir != DIR_W && pl.d[i].dir != DIR_N) return false;
-    static thread_local int simds = 0;
-    if (!simds) {
-        int dev = 0, cus = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        simds = 4 * (cus > 0 ? cus : 256);
-    }
-    return (long)pl.prefix[pl.ndirs] * F > simds;
+    return (long)pl.prefix[pl.ndirs] * F > 4L * device_cus();
 }
 
 void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st) {
@@ -438,366 +381,6 @@ void launch_paths(const Geometry& g, const PathLaunch& pl, int F, hipStream_t st
         if (g.D < 512) hipLaunchKernelGGL((k_paths<8, true>), grid, dim3(256), 0, st, g, pl);
         else hipLaunchKernelGGL((k_paths<8, false>), grid, dim3(256), 0, st, g, pl);
     }
-}
-
-// ------------------------------------------------------------------------------------------
-// Row-synchronous sweeps (batched MODE_HH; SweepArgs in sdr_internal.hpp).
-//
-// A workgroup owns a tile of kSweepOwn * cols columns of a frame and walks its rows in path order (up:
-// bottom to top with N, NE, NW; down: top to bottom with SE, SW).  Its own waves (1..kSweepOwn)
-// hold cols (sweep_cols) contiguous columns each; a column's path costs stay in the wave's registers from
-// row to row, so per row the wave reads each cost word once for all its directions, runs path_step
-// per direction and writes the saturated sum of them as one record.  A diagonal's predecessor one
-// column to the left ("A": NE, SE) or right ("B": NW, SW) in the neighbouring wave comes through
-// LDS (one barrier per row).  Across tiles: wave 0 recomputes diagonal A over the cols columns
-// left of the tile, wave kSweepOwn + 1 diagonal B over those right of it.  A halo column whose
-// predecessor lies outside the workgroup goes wrong, and the error moves one column inwards per
-// row, so the halo feeds the tile exact values for cols - 1 rows (sweep_cols); every cols - 1 rows
-// the halo waves reload their state from the neighbour tiles, which
-// publish their boundary columns' path costs through a global ring (system-coherent sc1 stores,
-// then a row counter; the reader polls the counter).  Every tile of a frame in flight must be
-// resident (sweep_shape sizes the grid from the occupancy; the engine never has two sweeps in
-// flight), and a wait gives up after a.spin polls with *err set: the batch's frames are then
-// overwritten as INVALID after the post-filter (launch_sweep_verdict) and the handle's status
-// reports SDR_ERR_DEVICE.  Residency assumes this process has the device to itself: another
-// process's persistent kernel holding CUs for longer than the spin budget makes the wait give up.
-// Bytes per cell: one C read (+ 2 / kSweepOwn for the halos) and one record write for
-// the pass (k_paths: one of each per direction); the fused WTA pass then reads one record for
-// them instead of one per direction.
-// ------------------------------------------------------------------------------------------
-
-// path_step's delta (wave minimum + P2, both halves) of a path-cost vector
-template <int K>
-__device__ __forceinline__ uint32_t delta_of(const Regs<K>& L, uint32_t P2x2) {
-    uint32_t m = kMaxPair;
-#pragma unroll
-    for (int i = 0; i < K; i++) m = pk_min(m, L.r[i]);
-    const uint32_t m16 = (uint32_t)__builtin_elementwise_min((unsigned short)(m & 0xffffu),
-                                                              (unsigned short)(m >> 16));
-    return wave_min_u32(m16) * 0x00010001u + P2x2;
-}
-
-template <int DPL, bool PAD, bool UP>
-__global__ __launch_bounds__(64 * kSweepWaves) void k_sweep(Geometry g, SweepArgs a, int F) {
-    constexpr int K = DPL / 2, NC = sweep_cols(DPL, UP), NWV = kSweepWaves, NO = kSweepOwn, RS = NC - 1;
-    constexpr int TILE = NC * NO;
-    static_assert(RS < NC, "a halo of NC columns feeds the tile exact values for NC - 1 rows");
-    // the row's wave minima reduced together (wave_deltas) except where their registers would
-    // spill (the padded D = 144..240 down pass: 168 VGPRs and 16 B of scratch a lane)
-#ifndef SDR_SWEEP_BATCH
-#define SDR_SWEEP_BATCH 1
-#endif
-    constexpr bool BATCH = SDR_SWEEP_BATCH && !(PAD && DPL == 4 && !UP);
-    constexpr int RING = 2;  // cost rows in registers: row k in slot k % 2, loaded a row (~2 us) ahead
-    __shared__ uint32_t xA[2][NWV][64 * K];  // row parity, wave: diagonal A of its last column
-    __shared__ uint32_t xB[2][NWV][64 * K];  // diagonal B of its first column
-    __shared__ uint32_t dA[2][NWV], dB[2][NWV];
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int slot = blockIdx.x / a.ntiles, tile = blockIdx.x - slot * a.ntiles;
-    const int W1 = g.W1, H = g.H, D = g.D;
-    const int tx0 = tile * TILE;
-    const bool lhalo = wv == 0, rhalo = wv == NWV - 1, own = !lhalo && !rhalo;
-    const int x0 = lhalo ? tx0 - NC : rhalo ? tx0 + TILE : tx0 + (wv - 1) * NC;
-    const int ncol = lhalo ? (tile > 0 ? NC : 0) : max(0, min(NC, W1 - x0));
-    const bool has_left = tile > 0, has_right = tile + 1 < a.ntiles;
-    const bool active = !PAD || lane * DPL < D;
-    const int lw = PAD ? min(lane, D / DPL - 1) : lane;
-    const uint32_t lofs = (uint32_t)(lw * DPL * 2);
-    const uint32_t P1x2 = splat16(g.P1), P2x2 = splat16(g.P2);
-    const uint32_t fresh = active ? 0u : kMaxPair;  // a chain's predecessor outside the image
-    const size_t ew = (size_t)D / 2;                // words of one column's path costs
-    // the ring entry of tile t, side (0: its first own columns' B, 1: its last own columns' A), parity
-    auto edge_at = [&](int t, int side, int parity) {
-        return a.edge + ((((size_t)slot * a.ntiles + t) * 2 + side) * 2 + parity) * NC * ew + (size_t)lw * K;
-    };
-    auto flag = [&](int t, int side) { return a.flags + ((size_t)slot * a.ntiles + t) * 2 + side; };
-    // after one timed-out wait the wave stops waiting (the launch then finishes, wrong but bounded)
-    bool gave_up = false;
-    auto wait = [&](const int* fl, int target) __attribute__((always_inline)) {
-        int n = 0;
-        while (!gave_up &&
-               __builtin_amdgcn_readfirstlane(__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-                   target) {
-            if (++n > a.spin) {
-                if (lane == 0) __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                gave_up = true;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the ring loads stay after the poll
-    };
-    Regs<K> fr;
-#pragma unroll
-    for (int i = 0; i < K; i++) fr.r[i] = fresh;
-
-    for (int f = slot, it = 0; f < F; f += a.nslots, it++) {
-        const int base = it * H;  // rows of this slot's earlier frames (the counters run on)
-        const char* cframe = (const char*)(a.C + (size_t)f * a.cs_fstride) + (ptrdiff_t)max(x0, 0) * D * 2;
-        char* rframe = (char*)(a.rec + (size_t)f * a.l_fstride + (size_t)max(x0, 0) * a.l_pix);
-        const size_t crow = (size_t)W1 * D * 2, rrow = (size_t)W1 * a.l_pix * 2;
-        auto yof = [&](int k) { return UP ? H - 1 - k : k; };
-        Regs<K> Lv[NC], La[NC], Lb[NC];
-        uint32_t dv[NC], da[NC], db[NC];
-#pragma unroll
-        for (int j = 0; j < NC; j++) {
-            Lv[j] = La[j] = Lb[j] = fr;
-            dv[j] = da[j] = db[j] = P2x2;
-        }
-        // this tile's boundary columns after row count-1 -> the ring, then the counter (the
-        // counter store waits for the data stores); data = false: the counter only
-        auto publish = [&](int count, bool data) __attribute__((always_inline)) {
-            const bool s0 = own && wv == 1 && has_left, s1 = own && wv == NO && has_right;
-            if (!s0 && !s1) return;
-            if (data && active) {
-                const int par = (count / RS) & 1;
-                uint32_t* e = edge_at(tile, s0 ? 0 : 1, par);
-#pragma unroll
-                for (int j = 0; j < NC; j++)
-#pragma unroll
-                    for (int i = 0; i < K; i++)
-                        __hip_atomic_store(e + j * ew + i, s0 ? Lb[j].r[i] : La[j].r[i], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no compiler motion across the wait
-            __builtin_amdgcn_s_waitcnt(0);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            if (lane == 0) __hip_atomic_store(flag(tile, s0 ? 0 : 1), count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        // a halo wave's state from the neighbour's boundary columns after row count-1
-        auto reload = [&](int count) __attribute__((always_inline)) {
-            if (lhalo && has_left) {
-                wait(flag(tile - 1, 1), count);
-                const uint32_t* e = edge_at(tile - 1, 1, (count / RS) & 1);
-#pragma unroll
-                for (int j = 0; j < NC; j++) {
-#pragma unroll
-                    for (int i = 0; i < K; i++)
-                        La[j].r[i] = active ? __hip_atomic_load(e + j * ew + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : kMaxPair;
-                    da[j] = delta_of<K>(La[j], P2x2);
-                }
-            }
-            if (rhalo && has_right) {
-                wait(flag(tile + 1, 0), count);
-                const uint32_t* e = edge_at(tile + 1, 0, (count / RS) & 1);
-#pragma unroll
-                for (int j = 0; j < NC; j++) {
-#pragma unroll
-                    for (int i = 0; i < K; i++)
-                        Lb[j].r[i] = active ? __hip_atomic_load(e + j * ew + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                            : kMaxPair;
-                    db[j] = delta_of<K>(Lb[j], P2x2);
-                }
-            }
-        };
-        Regs<K> cr[RING][NC];
-        auto load_row = [&](int k, Regs<K> (&dst)[NC]) __attribute__((always_inline)) {
-            const Rsrc r = rsrc_at(cframe + (size_t)yof(min(k, H - 1)) * crow);  // past the end: re-read the last row
-#pragma unroll
-            for (int j = 0; j < NC; j++) dst[j] = load_buf<K>(r, lofs + (uint32_t)(min(j, max(ncol - 1, 0)) * D * 2));
-        };
-        load_row(0, cr[0]);
-        // a new frame: the neighbours must be done reading this tile's ring entries of the last one
-        if (it > 0) {
-            if (lhalo && has_left) wait(flag(tile - 1, 1), base);
-            if (rhalo && has_right) wait(flag(tile + 1, 0), base);
-        }
-        // records of the wave's valid columns: a buffer resource clipped to them (the stores of
-        // columns past the image and of padding lanes fall outside it and are dropped), so the
-        // column loops carry no branches and the scheduler interleaves their independent steps
-        const uint32_t rec_bytes = ncol > 0 ? (uint32_t)((ncol - 1) * a.l_pix * 2 + D * 2) : 0u;
-        const uint32_t sofs = active ? lofs : 0x7fffffffu;
-        auto row = [&](const int k, auto sc) __attribute__((always_inline)) {
-            constexpr int s = decltype(sc)::value;
-            if (k > 0 && k % RS == 0) {
-                publish(base + k, true);
-                reload(base + k);
-            }
-            load_row(k + 1, cr[(s + 1) % RING]);
-            const Regs<K>(&c)[NC] = cr[s];
-            const bool first = k == 0;
-            Regs<K> outA = fr, outB = fr;
-            uint32_t doutA = P2x2, doutB = P2x2;
-            // diagonal A over the columns, from the column on the left (inA: the wave to the left,
-            // through LDS); descending, so La[j-1] is still the previous row's when column j takes it
-            // (BATCH: the columns' wave minima are reduced together after the loop, wave_deltas)
-            auto diag_a = [&](const Regs<K>& inA, uint32_t dinA, Regs<K>* sum) __attribute__((always_inline)) {
-                uint32_t m16[NC];
-#pragma unroll
-                for (int j = NC - 1; j >= 0; j--) {
-                    Regs<K> p = j > 0 ? La[j > 0 ? j - 1 : 0] : inA;
-                    uint32_t dp = j > 0 ? da[j > 0 ? j - 1 : 0] : dinA;
-                    uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    Regs<K> L;
-                    if constexpr (BATCH) {
-                        L = path_step_min16<K, PAD>(c[j], p, dp, P1x2, active, upr, dnr, m16[j]);
-                    } else {
-                        L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
-                        da[j] = dp;
-                    }
-                    La[j] = L;
-                    const bool o = j == ncol - 1;
-#pragma unroll
-                    for (int i = 0; i < K; i++) outA.r[i] = o ? L.r[i] : outA.r[i];
-                    if (sum) {
-#pragma unroll
-                        for (int i = 0; i < K; i++) sum[j].r[i] = UP ? pk_add_sat(sum[j].r[i], L.r[i]) : L.r[i];
-                    }
-                }
-                if constexpr (BATCH) wave_deltas<NC>(m16, da, P2x2);
-#pragma unroll
-                for (int j = 0; j < NC; j++) doutA = j == ncol - 1 ? da[j] : doutA;
-            };
-            // diagonal B from the column on the right (inB past the wave's last valid column)
-            auto diag_b = [&](const Regs<K>& inB, uint32_t dinB, Regs<K>* sum) __attribute__((always_inline)) {
-                uint32_t m16[NC];
-#pragma unroll
-                for (int j = 0; j < NC; j++) {
-                    const bool in = j + 1 < ncol;
-                    Regs<K> p;
-#pragma unroll
-                    for (int i = 0; i < K; i++) p.r[i] = in ? Lb[j + 1 < NC ? j + 1 : NC - 1].r[i] : inB.r[i];
-                    uint32_t dp = in ? db[j + 1 < NC ? j + 1 : NC - 1] : dinB;
-                    uint32_t upr = kMaxPair, dnr = kMaxPair;
-                    Regs<K> L;
-                    if constexpr (BATCH) {
-                        L = path_step_min16<K, PAD>(c[j], p, dp, P1x2, active, upr, dnr, m16[j]);
-                    } else {
-                        L = path_step<K, PAD, true>(c[j], p, dp, P1x2, P2x2, active, upr, dnr);
-                        db[j] = dp;
-                    }
-                    Lb[j] = L;
-                    if (sum) {
-#pragma unroll
-                        for (int i = 0; i < K; i++) sum[j].r[i] = pk_add_sat(sum[j].r[i], L.r[i]);
-                    }
-                }
-                if constexpr (BATCH) wave_deltas<NC>(m16, db, P2x2);
-                outB = Lb[0];
-                doutB = db[0];
-            };
-            if (own) {
-                // the predecessors of the wave's boundary columns (row k-1) from the neighbouring
-                // waves; past the image a fresh start
-                Regs<K> inA = fr, inB = fr;
-                uint32_t dinA = P2x2, dinB = P2x2;
-                if (!first) {
-#pragma unroll
-                    for (int i = 0; i < K; i++) inA.r[i] = xA[(k - 1) & 1][wv - 1][lane * K + i];
-                    dinA = dA[(k - 1) & 1][wv - 1];
-                    if (x0 + ncol < W1) {
-#pragma unroll
-                        for (int i = 0; i < K; i++) inB.r[i] = xB[(k - 1) & 1][wv + 1][lane * K + i];
-                        dinB = dB[(k - 1) & 1][wv + 1];
-                    }
-                }
-                Regs<K> sum[NC];
-                if constexpr (UP) {
-                    uint32_t m16[NC];
-#pragma unroll
-                    for (int j = 0; j < NC; j++) {
-                        uint32_t upr = kMaxPair, dnr = kMaxPair;
-                        if constexpr (BATCH)
-                            sum[j] = Lv[j] = path_step_min16<K, PAD>(c[j], Lv[j], dv[j], P1x2, active, upr, dnr, m16[j]);
-                        else
-                            sum[j] = path_step<K, PAD, true>(c[j], Lv[j], dv[j], P1x2, P2x2, active, upr, dnr);
-                    }
-                    if constexpr (BATCH) wave_deltas<NC>(m16, dv, P2x2);
-                }
-                diag_a(inA, dinA, sum);
-                diag_b(inB, dinB, sum);
-                const Rsrc rr = __builtin_amdgcn_make_buffer_rsrc(rframe + (size_t)yof(k) * rrow, (short)0,
-                                                                  (int)rec_bytes, 0x00020000);
-#pragma unroll
-                for (int j = 0; j < NC; j++) store_buf_nt<K>(rr, sofs + (uint32_t)(j * a.l_pix * 2), 0, sum[j]);
-            } else if (lhalo) {
-                // its first column's predecessor is outside the workgroup: any value (the error stays
-                // in the halo until the next reload)
-                if (ncol > 0) diag_a(fr, P2x2, nullptr);
-            } else {
-                if (ncol > 0) diag_b(fr, P2x2, nullptr);
-            }
-            // this row's boundary columns for the neighbouring waves (a wave without columns: a
-            // fresh start, the left halo of the first tile)
-#pragma unroll
-            for (int i = 0; i < K; i++) {
-                xA[k & 1][wv][lane * K + i] = outA.r[i];
-                xB[k & 1][wv][lane * K + i] = outB.r[i];
-            }
-            if (lane == 0) {
-                dA[k & 1][wv] = doutA;
-                dB[k & 1][wv] = doutB;
-            }
-            __syncthreads();
-        };
-        int k0 = 0;
-        for (; k0 + RING <= H; k0 += RING) unroll_rows(row, k0, std::make_integer_sequence<int, RING>{});
-        unroll_rows_tail(row, k0, H - 1, std::make_integer_sequence<int, RING - 1>{});
-        publish(base + H, false);  // the frame is done: the neighbours may start the next one
-    }
-}
-
-template <int DPL, bool PAD, bool UP>
-static int sweep_occupancy() {
-    static thread_local int per_cu = -1;
-    if (per_cu < 0) {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)k_sweep<DPL, PAD, UP>, 64 * kSweepWaves, 0) !=
-            hipSuccess)
-            n = 0;
-        per_cu = n;
-    }
-    return per_cu;
-}
-
-SweepShape sweep_shape(const Geometry& g, int F, bool up) {
-    SweepShape sh{0, 0, 0};
-    if (g.W1 <= 0 || F <= 0 || g.D > 256) return sh;  // four pairs per lane do not fit its registers
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int dpl = g.D <= 128 ? 2 : 4;
-    int occ;
-    if (dpl == 2) occ = up ? (g.D < 128 ? sweep_occupancy<2, true, true>() : sweep_occupancy<2, false, true>())
-                           : (g.D < 128 ? sweep_occupancy<2, true, false>() : sweep_occupancy<2, false, false>());
-    else occ = up ? (g.D < 256 ? sweep_occupancy<4, true, true>() : sweep_occupancy<4, false, true>())
-                  : (g.D < 256 ? sweep_occupancy<4, true, false>() : sweep_occupancy<4, false, false>());
-    sh.cols = sweep_cols(dpl, up);
-    const int tile = sh.cols * kSweepOwn;
-    sh.ntiles = (g.W1 + tile - 1) / tile;
-    sh.nslots = min(F, cus * occ / sh.ntiles);
-    return sh;
-}
-
-__global__ __launch_bounds__(256) void k_sweep_verdict(const int* __restrict__ err, int16_t* __restrict__ disp,
-                                                       size_t n, int F, int16_t invalid, int* __restrict__ mins,
-                                                       int* __restrict__ sticky) {
-    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
-        return;
-    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = tid; i < n * F; i += nth) disp[i] = invalid;
-    if (mins)
-        for (size_t i = tid; i < (size_t)F * kMinSlots; i += nth) mins[i] = invalid;
-    if (tid == 0) atomicOr(sticky, 1);
-}
-
-void launch_sweep_verdict(const int* err, int16_t* disp, size_t n, int F, int16_t invalid, int* mins,
-                          int* sticky, hipStream_t st) {
-    hipLaunchKernelGGL(k_sweep_verdict, dim3(1024), dim3(256), 0, st, err, disp, n, F, invalid, mins, sticky);
-}
-
-void launch_sweep(const Geometry& g, const SweepArgs& a, int F, hipStream_t st) {
-    const dim3 grid(a.nslots * a.ntiles), block(64 * kSweepWaves);
-#define SDR_SWEEP(DPL, PAD)                                                                   \
-    if (a.up) hipLaunchKernelGGL((k_sweep<DPL, PAD, true>), grid, block, 0, st, g, a, F);     \
-    else hipLaunchKernelGGL((k_sweep<DPL, PAD, false>), grid, block, 0, st, g, a, F);
-    if (g.D <= 128) {
-        if (g.D < 128) { SDR_SWEEP(2, true) } else { SDR_SWEEP(2, false) }
-    } else {
-        if (g.D < 256) { SDR_SWEEP(4, true) } else { SDR_SWEEP(4, false) }
-    }
-#undef SDR_SWEEP
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1151,13 +734,7 @@ static void launch_south_np(const Geometry& g, const PathLaunch& pl, const South
     if constexpr (DPL == 2) {
         // two columns per workgroup when the chains far outnumber what the chip holds at once
         // (short, latency-bound chains: the class path's 3WAY stripes), up to 5 paths
-        static thread_local int cus = 0;
-        if (!cus) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (cus <= 0) cus = 256;
-        }
+        const int cus = device_cus();
         if (a.npaths <= 5 && (long)pl.prefix[pl.ndirs] * F > 8L * cus) {
             int wgs = 0;
             for (int i = 0; i < pl.ndirs; i++) wgs += (pl.d[i].nchains + 1) / 2;

@@ -21,7 +21,7 @@ import numpy as np
 
 from ._lib import check, lib
 from .display import Display
-from .sgbm import MODE_SGBM_3WAY, StereoSGBM, _Q, createRightMatcher, torch
+from .sgbm import MODE_SGBM_3WAY, StereoSGBM, _Q, createRightMatcher, set_handle_stream, torch
 from .ximgproc import createDisparityWLSFilter
 
 
@@ -77,7 +77,7 @@ class LiveLoop:
                                        self.small_l.data_ptr(), self.small_r.data_ptr()))
         if ingest_events:
             ingest_events[1].record(stream)
-        check(L.sdr_sgbm_set_stream(self.left._h, s))
+        set_handle_stream(self.left._h, self.left._device, stream)
         # computeDisparity + computeDepth: reprojectImageTo3D(half-res disparity, full-res Q)
         # (stereo_disparity.cpp:76-80), fused into the WLS filter's epilogue
         check(L.sdr_stereo_class_depth_device(self.left._h, self.right._h, self.wls._h,
@@ -136,7 +136,7 @@ class CloudEmit:
         check(L.sdr_bgr2gray_device(sbs.data_ptr(), W, H, row, self.gray_l.data_ptr(), W, F, s))
         check(L.sdr_bgr2gray_device(sbs.data_ptr() + W * 3, W, H, row, self.gray_r.data_ptr(), W, F, s))
         # sgbm->compute -> convertTo(1/16) -> reprojectImageTo3D(handleMissing)  (:111-116)
-        check(L.sdr_sgbm_set_stream(self.m._h, s))
+        set_handle_stream(self.m._h, self.m._device, stream)
         check(L.sdr_sgbm_compute_reproject_device(self.m._h, self.gray_l.data_ptr(), self.gray_r.data_ptr(),
                                                   W, H, W, W * H, F, self.disp.data_ptr(), _Q(self.Q), 1,
                                                   self.xyz.data_ptr()))

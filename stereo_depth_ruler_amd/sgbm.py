@@ -32,7 +32,8 @@ MODE_SGBM, MODE_HH, MODE_SGBM_3WAY, MODE_HH4 = 0, 1, 2, 3
 UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
 # SDR_KERNEL_* (include/sdr/sdr.h)
 (KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATHS, KERNEL_WTA_LR, KERNEL_MEDIAN, KERNEL_SPECKLE,
- KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP, KERNEL_WLS_PREP, KERNEL_FGS, KERNEL_WLS_FINAL) = range(12)
+ KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP, KERNEL_WLS_PREP, KERNEL_FGS, KERNEL_WLS_FINAL,
+ KERNEL_SWEEP_DOWN) = range(13)
 DEBUG_SWEEP_SPIN = 1  # sdr_sgbm_debug_knob
 
 
@@ -42,6 +43,12 @@ def _is_cuda(x) -> bool:
 
 def _cstream(device_index: int):
     return ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
+
+
+def set_handle_stream(h, device_index: int, stream=None):
+    """Points a matcher handle at `stream` (default: the current stream of the device)."""
+    s = stream if stream is not None else torch.cuda.current_stream(device_index)
+    check(lib().sdr_sgbm_set_stream(h, ctypes.c_void_p(s.cuda_stream)))
 
 
 def _Q(Q) -> ctypes.Array:
@@ -173,7 +180,7 @@ class StereoSGBM:
         out = disp if disp is not None else torch.empty((f, h, w), dtype=torch.int16, device=left.device)
         if out.numel() != f * h * w or out.dtype != torch.int16 or not out.is_contiguous():
             raise SDRError(-1, "disp must be a contiguous int16 tensor of the input shape")
-        check(lib().sdr_sgbm_set_stream(self._h, _cstream(self._device)))
+        set_handle_stream(self._h, self._device)
         check(lib().sdr_sgbm_compute_device(self._h, left.data_ptr(), right.data_ptr(), w, h, w,
                                             w * h, f, out.data_ptr(), w, w * h))
         return out[0] if squeeze and disp is None else out
@@ -193,7 +200,7 @@ class StereoSGBM:
         out = disp if disp is not None else torch.empty((f, h, w), dtype=torch.int16, device=left.device)
         if out.numel() != f * h * w or out.dtype != torch.int16 or not out.is_contiguous():
             raise SDRError(-1, "disp must be a contiguous int16 tensor of the input's (F, H, W)")
-        check(lib().sdr_sgbm_set_stream(self._h, _cstream(self._device)))
+        set_handle_stream(self._h, self._device)
         check(lib().sdr_sgbm_compute_device_cn(self._h, left.data_ptr(), right.data_ptr(), w, h, 3, w * 3,
                                                w * h * 3, f, out.data_ptr(), w, w * h))
         return out[0] if squeeze and disp is None else out
@@ -212,7 +219,7 @@ class StereoSGBM:
             disp = torch.empty((f, h, w), dtype=torch.int16, device=left.device)
         if xyz is None:
             xyz = torch.empty((f, h, w, 3), dtype=torch.float32, device=left.device)
-        check(lib().sdr_sgbm_set_stream(self._h, _cstream(self._device)))
+        set_handle_stream(self._h, self._device)
         check(lib().sdr_sgbm_compute_reproject_device(
             self._h, left.data_ptr(), right.data_ptr(), w, h, w, w * h, f, disp.data_ptr(), _Q(Q),
             int(bool(handleMissingValues)), xyz.data_ptr()))

@@ -154,6 +154,35 @@ def test_bench_gpus2_nccl_needs_two_gpus():
     assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
 
 
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_bench_rccl_world1(config):
+    """The RCCL data path executed on the one-GPU box: bench.py under
+    torch.distributed.run --nproc-per-node 1 with --dist-world1 initialises the nccl (RCCL)
+    process group on the GPU, runs the per-step dist.gather of device tensors to rank 0, the
+    status exchanges and the end-to-end gather check -- the same calls the 8-GPU run makes."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"), "--gpus", "1",
+           "--dist-world1", "--config", config, "--steps", "20", "--warmup", "3", "--status-every", "4",
+           "--no-cpu-baseline", "--no-kernel-timing"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["value"] > 0
+    assert out["ranks"]["backend"] == "nccl (RCCL)" and out["ranks"]["world_size_seen"] == 1
+    assert out["gather_check"]["ok"] and out["gather_check"]["ranks"] == 1
+    assert "RCCL gather" in out["config"]["parallelism"]
+
+
 def _failing_worker(rank, world, port, q):
     """Rank 1 asks the real engine for numDisparities = 20 (SDR_ERR_NUMDISP, OpenCV's assert)."""
     import sys

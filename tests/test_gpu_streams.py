@@ -59,3 +59,38 @@ def test_stream_switch_with_pending_work(mode, D, F, oracle):
     p = oracle.make_params(*args)
     assert np.array_equal(refs[0][0].cpu().numpy(), oracle.sgbm_compute(Ls[0], Rs[0], p))
     m.close()
+
+
+def test_caller_stream_destroyed_after_switching_away(oracle):
+    """ADVICE r4 / sdr.h: a caller's stream must outlive the handle's use of it (HIP does not
+    validate a destroyed stream's handle: an event recorded on one, or waited on after being
+    recorded there, crashes the process -- measured on MI355X in round 5, so no engine-side check
+    can catch the misuse).  The supported order: work on a caller's stream, move the handle off it
+    (another stream, or reset_stream), destroy the stream, keep using the handle -- bit-exact, and
+    close() works."""
+    import ctypes
+
+    from stereo_depth_ruler_amd._lib import check, lib
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    H, W, D = 120, 320, 64
+    Ls, Rs = S.make_batch(1, H, W, D, seed0=77)
+    dev = torch.device("cuda", 0)
+    L, R = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    args = (0, D, 5, 600, 2400, 1, 63, 12, 0, 2, sdr.MODE_SGBM)
+    ref = oracle.sgbm_compute(Ls[0], Rs[0], oracle.make_params(*args))
+    m = sdr.StereoSGBM.create(*args)
+    for leave in ("set_stream", "reset_stream"):
+        raw = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+        with torch.cuda.stream(torch.cuda.ExternalStream(raw.value, device=dev)):
+            out = m.compute(L, R)
+        if leave == "set_stream":  # the caller's next stream, as compute() on it would
+            check(lib().sdr_sgbm_set_stream(m._h, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+        else:
+            check(lib().sdr_sgbm_reset_stream(m._h))
+        assert hip.hipStreamDestroy(raw) == 0
+        assert np.array_equal(out[0].cpu().numpy(), ref)
+        for _ in range(2):
+            assert np.array_equal(m.compute(L, R)[0].cpu().numpy(), ref)
+    m.close()

@@ -105,6 +105,31 @@ def test_sweep_timeout_poisons_batch_and_reports(oracle):
     m.close()
 
 
+def test_sweep_timeout_reported_by_next_call(oracle):
+    """A caller that never polls sdr_sgbm_last_status still hears of a timed-out sweep:
+    the next compute call on the handle returns SDR_ERR_DEVICE without running, the status is then
+    clean, and the call after is bit-exact."""
+    F, H, W, D = 16, 96, 1700, 48
+    args = (0, D, 5, 600, 2400, 1, 63, 10, 0, 2, sdr.MODE_HH)
+    Ls, Rs = _batch("textured", F, H, W, D, 41)
+    dev = torch.device("cuda", 0)
+    Ld, Rd = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    m = sdr.StereoSGBM.create(*args)
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 1)
+    bad = m.compute(Ld, Rd).cpu().numpy()  # synchronises: the status copy has landed
+    assert (bad == -16).all()
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 0)
+    with pytest.raises(sdr.SDRError) as ei:
+        m.compute(Ld, Rd)
+    assert ei.value.code == -6
+    m.check_status()  # reported by the call: clean
+    good = m.compute(Ld, Rd).cpu().numpy()
+    m.check_status()
+    p = oracle.make_params(*args)
+    assert np.array_equal(good[F - 1], oracle.sgbm_compute(Ls[F - 1], Rs[F - 1], p))
+    m.close()
+
+
 def test_two_handles_two_streams_concurrent_sweeps(oracle):
     """Two matchers on two streams each enqueue 8-frame MODE_HH batches back to back without a
     synchronisation in between: their sweeps are chained per device (never two in flight), and

@@ -184,28 +184,18 @@ def load_traffic(kernel_tag):
         return None
 
 
-def stream_probe(dev, mib=2048, iters=10):
-    """This box's streaming rate: a device-to-device copy of a 2 GiB buffer (read + write bytes
-    over time), the ceiling a bandwidth-bound kernel of the same box can be held against --
-    the box-to-box spread of the HBM rate shows up here and in `roofline.achieved` alike."""
-    import torch
+def stream_probe(dev, mib=2048, iters=20):
+    """This box's streaming rate (sdr_stream_probe: a copy with the path kernels' 16-byte loads and
+    non-temporal stores over 2 GiB, read + write bytes), the ceiling a bandwidth-bound kernel of
+    the same box can be held against: box-to-box spread shows up here and in `achieved` alike."""
+    import ctypes
 
-    n = mib << 20
-    a_ = torch.empty(n, dtype=torch.uint8, device=dev)
-    b_ = torch.empty(n, dtype=torch.uint8, device=dev)
-    a_.fill_(1)
-    b_.copy_(a_)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        b_.copy_(a_)
-    e1.record()
-    torch.cuda.synchronize()
-    s_ = e0.elapsed_time(e1) / 1e3 / iters
-    del a_, b_
-    return {"gbs": round(2 * n / s_ / 1e9, 1), "what": f"torch device copy of {mib} MiB (read + write bytes), "
-                                                        f"mean of {iters} back to back"}
+    from stereo_depth_ruler_amd._lib import check, lib
+
+    g = ctypes.c_double()
+    check(lib().sdr_stream_probe(dev.index, mib << 20, iters, ctypes.byref(g)))
+    return {"gbs": round(g.value, 1), "what": f"sdr_stream_probe: {iters} copies of {mib} MiB (16-B loads, "
+                                              f"non-temporal stores), read + write bytes"}
 
 
 def free_port() -> int:
@@ -343,8 +333,8 @@ def main():
                     "median": _sg.KERNEL_MEDIAN, "speckle": _sg.KERNEL_SPECKLE,
                     "reproject": _sg.KERNEL_REPROJECT, "k_sweep": _sg.KERNEL_SWEEP,
                     "k_sweep_down": _sg.KERNEL_SWEEP_DOWN,
-                    "k_wls_prep": _sg.KERNEL_WLS_PREP, "fgs_pass": _sg.KERNEL_FGS,
-                    "k_wls_final": _sg.KERNEL_WLS_FINAL}
+                    "k_wls_prep": _sg.KERNEL_WLS_PREP, "fgs_coef": _sg.KERNEL_FGS_COEF,
+                    "fgs_pass": _sg.KERNEL_FGS, "k_wls_final": _sg.KERNEL_WLS_FINAL}
 
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
     D, mode = args[1], args[10]

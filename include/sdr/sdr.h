@@ -192,16 +192,18 @@ typedef struct sdr_wls_params {
     int num_iter;                   /* FGS iterations (3) */
     int left_offset, right_offset, top_offset, bottom_offset;
     int min_disp;                   /* outside-ROI value is 16*(min_disp-1) */
-    int fgs_solver;                 /* SDR_FGS_PCR (default) or SDR_FGS_THOMAS (below) */
+    int fgs_solver;                 /* SDR_FGS_THOMAS (default) or SDR_FGS_PCR (below) */
 } sdr_wls_params;
 
 /* Solver of the FGS line systems (I + lambda*L) u = f.  ximgproc runs the sequential Thomas
- * elimination; SDR_FGS_THOMAS reproduces it operation for operation (bit-exact with
- * oracle/wls_oracle.c fgs_line), one lane per image line.  SDR_FGS_PCR (default) solves the same
- * systems by parallel cyclic reduction, a workgroup per line, with the diagonal carried as the
- * row sum: it is ~200x closer to the exact solution than the sequential sweep in float32 and
- * differs from it by at most 1 int16 level in the WLS output (tests/test_gpu_wls.py); lines of at
- * most 4096 samples. */
+ * elimination; SDR_FGS_THOMAS (the default since round 5) reproduces it operation for operation
+ * (bit-exact with oracle/wls_oracle.c fgs_line), one lane per image line, the later passes'
+ * elimination coefficients computed alongside the first.  SDR_FGS_PCR solves the same systems by
+ * parallel cyclic reduction, a workgroup per line, with the diagonal carried as the row sum: it is
+ * ~200x closer to the exact solution than the sequential sweep in float32, and on the reference's
+ * own frames within 1 int16 level of it, but where the confidence map is sparse the sequential
+ * sweep's own float error reaches hundreds of levels (profiles/r5_pcr_vs_thomas.json), so PCR is
+ * not a drop-in there; lines of at most 4096 samples. */
 enum { SDR_FGS_PCR = 0, SDR_FGS_THOMAS = 1 };
 
 /* cv::ximgproc::createDisparityWLSFilter(matcher_left) (stereo_disparity.cpp:11): fills the
@@ -390,9 +392,10 @@ enum {
     SDR_KERNEL_SWEEP = 8,    /* k_sweep: batched MODE_HH's up pass (N, NE, NW) */
     /* the class path's WLS filter (sdr_stereo_class_*), recorded on the left matcher's handle */
     SDR_KERNEL_WLS_PREP = 9, /* k_wls_prep (or k_wls_disc + k_wls_conf past 4096 ROI columns) */
-    SDR_KERNEL_FGS = 10,     /* one FGS pass: k_fgs_pcr, or k_fgs_sweep (+ its transposes) */
+    SDR_KERNEL_FGS = 10,     /* one FGS pass: k_fgs_pcr, or k_fgs_th (SDR_FGS_THOMAS) */
     SDR_KERNEL_WLS_FINAL = 11, /* k_wls_final (+ /16 + computeDepth epilogue) */
-    SDR_KERNEL_SWEEP_DOWN = 12 /* batched MODE_HH's down pass (SE, SW): timed apart from the up pass */
+    SDR_KERNEL_SWEEP_DOWN = 12, /* batched MODE_HH's down pass (SE, SW): timed apart from the up pass */
+    SDR_KERNEL_FGS_COEF = 13 /* SDR_FGS_THOMAS: the coefficient jobs of a filter's passes (one launch) */
 };
 int sdr_sgbm_enable_timing(sdr_sgbm* h, int level);
 int sdr_sgbm_last_timing(const sdr_sgbm* h, float* cost_ms, float* paths_ms, float* post_ms);
@@ -415,6 +418,11 @@ int sdr_sgbm_debug_knob(sdr_sgbm* h, int knob, int value);
 /* Device self-test of the cross-lane primitives the kernels rely on (DPP wave shifts,
  * permlane swaps); fills 4 failure counters, all zero on a healthy gfx950. */
 int sdr_selftest_wave_ops(int* failures4);
+
+/* The device's streaming rate: `iters` back-to-back copies of a `bytes` buffer (16-byte loads,
+ * non-temporal stores: the path kernels' read + write pattern), read + write bytes per second in
+ * GB/s.  bench.py records it beside the dominant kernel's rate (box-to-box spread). */
+int sdr_stream_probe(int device, size_t bytes, int iters, double* gbs);
 
 /* Diagnostics: synchronously copy an internal buffer of the last compute to host memory.
  * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,

@@ -334,7 +334,7 @@ public:
     void setLRCthresh(int v) { p_.lrc_thresh = v; push(); }
     int getDepthDiscontinuityRadius() const { return p_.depth_discontinuity_radius; }
     void setDepthDiscontinuityRadius(int v) { p_.depth_discontinuity_radius = v; push(); }
-    // engine extension: FGS line solver, SDR_FGS_PCR (default) or SDR_FGS_THOMAS (sdr.h)
+    // engine extension: FGS line solver, SDR_FGS_THOMAS (default) or SDR_FGS_PCR (sdr.h)
     int getFgsSolver() const { return p_.fgs_solver; }
     void setFgsSolver(int v) { p_.fgs_solver = v; push(); }
 

@@ -252,9 +252,9 @@ def wls_confidence(dl, dr, p: WlsParams):
     return out
 
 
-def fgs_filter(guide, img, lambda_, sigma_color, attenuation=0.25, num_iter=3, solver=FGS_PCR):
-    """FastGlobalSmootherFilter; solver FGS_PCR (the engine's default) or FGS_THOMAS (ximgproc's
-    sequential sweep)."""
+def fgs_filter(guide, img, lambda_, sigma_color, attenuation=0.25, num_iter=3, solver=FGS_THOMAS):
+    """FastGlobalSmootherFilter; solver FGS_THOMAS (ximgproc's sequential sweep, the engine's
+    default) or FGS_PCR."""
     guide = np.ascontiguousarray(guide, np.uint8)
     out = np.array(img, dtype=np.float32, copy=True, order="C")
     h, w = out.shape

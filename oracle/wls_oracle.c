@@ -30,7 +30,7 @@ void orc_wls_params_for_sgbm(int minDisparity, int numDisparities, int blockSize
     p->roi_w = width - l - r;
     p->roi_h = height;
     p->min_disp = minDisparity;
-    p->fgs_solver = ORC_FGS_PCR;
+    p->fgs_solver = ORC_FGS_THOMAS;
 }
 
 void orc_fgs_lut(double sigma_color, float* lut) {

@@ -53,7 +53,7 @@ typedef struct {
     int num_iter;              /* FGS default 3 */
     int roi_x, roi_y, roi_w, roi_h; /* valid ROI of the left disparity map */
     int min_disp;              /* left matcher minDisparity (outside-ROI value 16*(min_disp-1)) */
-    int fgs_solver;            /* ORC_FGS_PCR (default) or ORC_FGS_THOMAS */
+    int fgs_solver;            /* ORC_FGS_THOMAS (default: ximgproc's order) or ORC_FGS_PCR */
 } orc_wls_params;
 
 enum { ORC_FGS_PCR = 0, ORC_FGS_THOMAS = 1 };

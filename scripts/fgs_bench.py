@@ -1,5 +1,6 @@
 """FGS (fastGlobalSmootherFilter) device timing on the class path's shape: two right-hand sides of
-one 560x360 ROI (the C0/C4 WLS filter), both solvers.  python scripts/fgs_bench.py [iters]"""
+one 560x360 ROI (the C0/C4 WLS filter), both solvers.
+python scripts/fgs_bench.py [iters] [--lib PATH] [--thomas-only]"""
 import sys
 import time
 
@@ -9,13 +10,22 @@ import torch
 sys.path.insert(0, __file__.rsplit("/", 2)[0])
 from stereo_depth_ruler_amd.ximgproc import FGS_PCR, FGS_THOMAS, fastGlobalSmootherFilter  # noqa: E402
 
-it = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+args = sys.argv[1:]
+if "--lib" in args:
+    from stereo_depth_ruler_amd import _lib  # noqa: E402
+
+    i = args.index("--lib")
+    _lib.use_library(args[i + 1])
+    del args[i:i + 2]
+only = "--thomas-only" in args
+args = [a for a in args if a != "--thomas-only"]
+it = int(args[0]) if args else 50
 rng = np.random.default_rng(0)
 h, w = 360, 560
 dev = torch.device("cuda", 0)
 g = torch.from_numpy(rng.integers(0, 256, (h, w)).astype(np.uint8)).to(dev)
 x = torch.from_numpy((rng.random((2, h, w)) * 1000).astype(np.float32)).to(dev)
-for solver, name in ((FGS_PCR, "pcr"), (FGS_THOMAS, "thomas")):
+for solver, name in ((FGS_PCR, "pcr"), (FGS_THOMAS, "thomas"))[1 if only else 0:]:
     for _ in range(3):
         fastGlobalSmootherFilter(g, x, 8000.0, 1.1, solver=solver)
     torch.cuda.synchronize()

@@ -566,9 +566,15 @@ __global__ __launch_bounds__(64 * (1 + kSouthConsumers)) void k_south_wta(Geomet
     }
     const char* lbase = (const char*)(a.L + (size_t)f * pl.l_fstride + ((size_t)ch.y0 * W1 + ch.x0) * pl.l_pix);
     // blocks past the chain's last one re-read that block (L2 hits), not the buffers' slack
+    // a block whose rows all lie before the chain's first output row (a 3WAY stripe's overlap
+    // rows: recurred through by the producer, never output) reads its records from an empty
+    // resource -- zeros, no memory traffic, no branch (its sums are never output)
     auto oload = [&](int q, int blk, int ps) __attribute__((always_inline)) {
-        return load_buf<WK, kLoadNT>(rsrc_at(lbase + (ptrdiff_t)min(blk, nblk - 1) * bstepb),
-                                     lofs[ps] + (uint32_t)(q * D * 2));
+        const bool need = blk * RB + RB > ch.kwrite;
+        const Rsrc r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<char*>(lbase + (ptrdiff_t)min(blk, nblk - 1) * bstepb), (short)0, need ? 0x7fffffff : 0,
+            0x00020000);
+        return load_buf<WK, kLoadNT>(r, lofs[ps] + (uint32_t)(q * D * 2));
     };
     // rows before kw belong to the previous 3WAY stripe: recurred through, never output
     const int kw = ch.kwrite;

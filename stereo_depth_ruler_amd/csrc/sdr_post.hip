@@ -669,6 +669,49 @@ __global__ void k_selftest(int* fails, uint32_t seed) {
     if (mu != e) atomicAdd(&fails[3], 1);
 }
 
+// The streaming probe (sdr_stream_probe): a grid-stride copy with 16-byte loads and non-temporal
+// stores -- k_paths' own data flow, one read and one write per byte of a cost row -- over buffers
+// larger than the caches, so a bench line can put the box's streaming rate beside its kernels'.
+typedef unsigned int probe_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_probe(const probe_u32x4* __restrict__ src,
+                                                      probe_u32x4* __restrict__ dst, size_t n) {
+    const size_t nth = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth)
+        __builtin_nontemporal_store(src[i], &dst[i]);
+}
+
+int stream_probe(size_t bytes, int iters, double* gbs) {
+    probe_u32x4 *a = nullptr, *b = nullptr;
+    const size_t n = bytes / 16;
+    if (hipMalloc((void**)&a, n * 16) != hipSuccess) return -1;
+    if (hipMalloc((void**)&b, n * 16) != hipSuccess) {
+        (void)hipFree(a);
+        return -1;
+    }
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = -1;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
+        hipEventCreate(&e1) == hipSuccess && hipMemsetAsync(a, 1, n * 16, st) == hipSuccess) {
+        const dim3 grid(device_cus() * 8), blk(256);
+        hipLaunchKernelGGL(k_stream_probe, grid, blk, 0, st, a, b, n);  // warm
+        (void)hipEventRecord(e0, st);
+        for (int i = 0; i < iters; i++) hipLaunchKernelGGL(k_stream_probe, grid, blk, 0, st, a, b, n);
+        (void)hipEventRecord(e1, st);
+        float ms = 0.0f;
+        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.0f) {
+            *gbs = 2.0 * (double)(n * 16) * iters / (ms * 1e-3) / 1e9;
+            rc = 0;
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return rc;
+}
+
 int selftest_wave_ops(int* failures) {
     int* d = nullptr;
     if (hipMalloc(&d, 4 * sizeof(int)) != hipSuccess) return -1;

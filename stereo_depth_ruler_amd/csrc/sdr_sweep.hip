@@ -47,13 +47,25 @@ constexpr int kDppRowShr1 = 0x111;  // lane i <- lane i-1 within its 16-lane row
 constexpr int kDppRowShl1 = 0x101;  // lane i <- lane i+1 within its 16-lane row
 
 // slots (columns per lane row) of the own waves and the halo waves of a pass
+#ifndef SDR_SW_UP_MO
+#define SDR_SW_UP_MO 2
+#endif
+#ifndef SDR_SW_UP_MH
+#define SDR_SW_UP_MH 2
+#endif
+#ifndef SDR_SW_DN_MO
+#define SDR_SW_DN_MO 1
+#endif
+#ifndef SDR_SW_DN_MH
+#define SDR_SW_DN_MH 2
+#endif
 template <int DW, bool UP>
 struct SwShape {
     // the up pass keeps N, NE, NW of M = 2 columns per lane row in registers; the down pass adds
     // the E, W and up records of two rows in flight and the WTA, so its own waves hold one
     // column per lane row, and its halo waves (one diagonal each, no records) two
-    static constexpr int MO = UP ? 2 : 1;
-    static constexpr int MH = 2;
+    static constexpr int MO = UP ? SDR_SW_UP_MO : SDR_SW_DN_MO;
+    static constexpr int MH = UP ? SDR_SW_UP_MH : SDR_SW_DN_MH;
 };
 
 // the path recurrence of one pixel step on a 16-lane row: L = C + min(Lp, min(Lp[d-1], Lp[d+1]) +

@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -42,6 +43,10 @@
 namespace sdr {
 
 constexpr int kFgsLevels = 65026;  // 255^2 + 1 squared differences of two 8-bit gray levels
+
+// the sequential solver's k-major arrays keep their sample rows 16-byte aligned: line counts and
+// line lengths rounded up to 4 (frames fgs_pad4(w) * fgs_pad4(h) samples apart)
+__host__ __device__ __forceinline__ int fgs_pad4(int x) { return (x + 3) & ~3; }
 
 __device__ __forceinline__ int reflect101(int p, int len) {
     if (len == 1) return 0;
@@ -162,131 +167,567 @@ __global__ __launch_bounds__(256) void k_wls_conf(const int16_t* __restrict__ dl
 
 // FGS line solve, per line of n samples with weights C[k] = lut[(g[k] - g[k+1])^2] (0 at the
 // last sample):  (1 - lam*(C[k-1] + C[k])) u_k + lam*C[k-1] u_{k-1} + lam*C[k] u_{k+1} = f_k
-// (C = -w <= 0), Thomas forward elimination then back substitution, in the oracle's order:
+// (C = -w <= 0), Thomas forward elimination then back substitution, in the oracle's order
+// (oracle/wls_oracle.c fgs_line, ximgproc's fgs_filter.cpp sweep):
 //   k=0:  den = 1 - lam*C0;  t0 = lam*C0 / den;  u0 = u0 / den
 //   k>0:  a = lam*C[k-1];  c = lam*C[k];  den = (1 - c) - a*(1 + t[k-1]);
 //         t[k] = c / den;  u_k = (u_k - a*u_{k-1}) / den
 //   back: u_k = u_k - t[k]*u_{k+1}
+// The elimination coefficients (den, t) depend on the guide's weights and lambda only, not on the
+// right-hand sides: one launch of coefficient jobs computes them for every pass of a filter first
+// (the t recurrence, ~13 dependent operations a sample with its IEEE division, and 1/den beside
+// it), and the passes then run only the right-hand sides' recurrence, with the division x / den
+// done from the correctly rounded reciprocal r = 1/den:
+//   q0 = x*r,  rem = -fma(q0, den, -x) (exact),  q = fma(rem, r, q0)
+// which is the correctly rounded quotient (Markstein's theorem: r within half an ulp of 1/den and
+// q0 within an ulp of x/den; den >= 1 here) as long as nothing underflows: for 0 < |q0| < 2^-96 a
+// chunk runs again with real divisions; scripts/markstein_check.c finds no difference at or above
+// that threshold in 2e9 random pairs (den up to 2^60).  Five dependent operations a sample.
 //
-// Layout: a sweep runs over "k-major" arrays, element (line l, sample k) at k*nlines + l, so that
-// the 64 lanes of a wave (64 consecutive lines) touch 256 contiguous bytes per sample.  The row
-// pass therefore works on column-major copies and the column pass on row-major ones; k_transpose2
-// moves both right-hand sides between the two (LDS tiles).  Each lane walks its line with the
-// loads of the next PF samples in flight (register ring), so a step costs the dependent-division
-// latency of the t recurrence, not a memory round trip.
-constexpr int kFgsPF = 8;  // samples each lane loads ahead in the line solves
+// A pass of F frames x nl lines runs as a chain on one wave per workgroup (lane = line, LPB = 16,
+// 32 or 64 lines a workgroup), which touches nothing but LDS, with three helper waves:
+//   wave 0    the solver: the recurrence of its LPB lines sample by sample, each sample's operands
+//             read from the LDS ring kThPF samples ahead (ds_read latency off the chain), each
+//             result written to an LDS row for the writer
+//   waves 1-2 loaders: LDS-DMA (global_load_lds_dwordx4, 1 KiB a wave-instruction) of the next
+//             chunks (CH = 1024 / LPB samples x LPB lines of every operand stream) into a ring of
+//             kThNB buffers, up to kThNB - 2 chunks in flight
+//   wave 3    the writer: every global store of the pass -- the forward values (k-major, in place)
+//             and the results (line-major: the next pass's k-major layout, the transpose between
+//             passes done by reading the rows transposed; or k-major into the two outputs)
+// One s_barrier per chunk orders them: chunk c + 2 has landed (loaders' counted vmcnt), the solver
+// is done with chunk c - 1's buffer and has written chunk c's rows before the barrier that ends
+// iteration c.  Measured at 640x360 (a 560x360 ROI, two right-hand sides): 64 lines a workgroup
+// with the solver storing its own results, 96 us a pass; 16 lines, 77 us; 16 lines with the
+// stores on the writer wave, 39 us (the solver's stores queued behind the loaders' DMA in the
+// CU's memory pipeline: a variant without them ran 45 us at 77).
+// Layout: every k-major array (element (line l, sample k) at k * st + l, st = nl rounded up to 4)
+// has 16-byte aligned sample rows, which the 16-byte DMA needs; the frames are fs apart.
+constexpr int kThNB = 5;          // LDS ring buffers
+constexpr int kThPF = 8;          // the solver's LDS lookahead (samples)
+constexpr int kThBuf = 1024 * 24; // a chunk (1024 line-samples) of the largest stream set
+template <int LPB, int ES> struct ThRows {
+    // the solver's back-substitution rows: CH samples x LPB lines, double-buffered; the row stride
+    // S (dwords) is = E * LPB / 16 (mod 64), so that the writer's transposed reads (CH samples of
+    // 64 / CH lines a wave-instruction) fall on distinct banks
+    static constexpr int CH = 1024 / LPB, E = ES / 4;
+    static constexpr int S = LPB * E + (64 - (LPB * E) % 64) % 64 + E * LPB / 16;
+    static constexpr int bytes = 2 * CH * S * 4;
+};
+constexpr int kThRows = ThRows<16, 8>::bytes;  // the rows area (the largest use)
+constexpr int kThLds = kThNB * kThBuf + kThRows;
+static_assert(ThRows<32, 8>::bytes <= kThRows && ThRows<64, 8>::bytes <= kThRows, "rows");
+static_assert(kThRows >= 2 * 1024 * 16, "the forward and job rows fit the rows area");
+static_assert(kThLds <= 160 * 1024, "one workgroup's LDS");
+constexpr int kFgsMaxJobs = 8;         // coefficient jobs in one launch
+constexpr size_t kFgsOverread = 4096;  // bytes past a k-major array the loaders may read (the
+                                       // last workgroup's lines beyond st, at the last sample)
+constexpr uint32_t kFgsTinyKey = 0x1EFFFFFFu;  // fgs_tiny_key(q) < this <=> 0 < |q| < 2^-96
 
-// The line solve has no per-sample branches: the second right-hand side is a template parameter,
-// the first sample uses the general step (with cprev = tprev = p = 0 it computes
-// den = (1 - c) - 0, t = c / den, p = (r - 0) / den: the k = 0 formulas, bit for bit), and only
-// the last, partial batch of PF samples checks the line's end.  The step's divisions are plain
-// IEEE divisions (a shared refined reciprocal was bit-exact too, and no faster: the sweep is not
-// bound by the division chain).
-template <bool U1>
-__global__ __launch_bounds__(64) void k_fgs_sweep(float* U0, float* U1p, const float* __restrict__ Cw,
-                                                   float* __restrict__ T, int nlines, int n,
-                                                   size_t fstride, float lam) {
-    constexpr int PF = kFgsPF;
-    const int l = blockIdx.x * 64 + threadIdx.x;
-    if (l >= nlines) return;
-    const size_t base = (size_t)blockIdx.y * fstride + l;
-    float* u0 = U0 + base;
-    float* u1 = U1 ? U1p + base : nullptr;
-    const float* cw = Cw + base;
-    float* t = T + base;
-    const size_t st = (size_t)nlines;
-    const int last = n - 1;
+// 2|q| - 1 as an integer (the sign bit shifted out): below kFgsTinyKey exactly when 0 < |q| < 2^-96
+// (+-0 wraps to the largest key); the minimum over a chunk decides the redo
+__device__ __forceinline__ uint32_t fgs_tiny_key(float q) { return __builtin_bit_cast(uint32_t, q) * 2u - 1u; }
+
+struct FgsCoefJob {
+    const float* Cw;  // the pass's weights, k-major
+    float4* coef;     // [F] frames of (a, den, 1/den, t), k-major
+    float* tt;        // [F] frames of t, k-major (the back substitution's stream)
+    float lam;
+    int nl, n;
+    int st;           // k-major sample stride (nl rounded up to 4)
+    int blocks;
+};
+
+struct FgsThArgs {
+    void* U;                // k-major right-hand sides: float, or float2 (two, interleaved); the
+                            // forward values are written back in place
+    const float4* coef;     // this pass's (a, den, 1/den, t) ...
+    const float* tt;        // ... and t
+    void* O;                // line-major results (same element type as U; line stride onp), or
+                            // null: ...
+    float* O0;              // ... k-major results split into two arrays (the last pass; sample
+    float* O1;              // stride ost, frames ofs apart)
+    int nl, n;
+    int st;                 // k-major sample stride of U, coef, tt
+    int onp;                // O's line stride (n rounded up to 4: the next pass's st)
+    size_t fs;              // frame stride of U, coef, tt, O
+    size_t ost, ofs;
+    int main_blocks;        // blocks of the pass itself; blocks past them run coefficient jobs
+    int njobs;
+    FgsCoefJob job[kFgsMaxJobs];
+};
+
+template <bool TWO> struct FgsRhs;
+template <> struct FgsRhs<true> {
+    typedef float2 T;
+    static __device__ __forceinline__ float x(const T& v) { return v.x; }
+    static __device__ __forceinline__ float y(const T& v) { return v.y; }
+    static __device__ __forceinline__ T make(float a, float b) { return make_float2(a, b); }
+};
+template <> struct FgsRhs<false> {
+    typedef float T;
+    static __device__ __forceinline__ float x(const T& v) { return v; }
+    static __device__ __forceinline__ float y(const T&) { return 0.0f; }
+    static __device__ __forceinline__ T make(float a, float) { return a; }
+};
+
+typedef __attribute__((address_space(3))) void* th_lds_ptr;
+typedef __attribute__((address_space(1))) void* th_glb_ptr;
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+template <int N> __device__ __forceinline__ void th_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// s_waitcnt lgkmcnt(0) alone: the solver's LDS rows are written before the barrier
+__device__ __forceinline__ void th_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
+// the workgroup barrier without the fence __syncthreads() carries (whose vmcnt(0) would drain the
+// loaders' DMA in flight); the empty asm keeps the compiler from moving LDS accesses across it
+__device__ __forceinline__ void th_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+#ifdef SDR_TH_STAMPS
+// diagnostic build only: s_memtime stamps of workgroup (0, 0) of one launch (scripts/th_stamps.py)
+__device__ unsigned long long* g_th_stamps;
+#define TH_STAMP(role, idx)                                                                       \
+    do {                                                                                          \
+        if (g_th_stamps && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 63) == 0)         \
+            g_th_stamps[(role) * 1024 + (idx)] = __builtin_amdgcn_s_memtime();                    \
+    } while (0)
+#else
+#define TH_STAMP(role, idx) \
+    do {                    \
+    } while (0)
+#endif
+
+// A loader wave's share (lw = 0, 1) of one stream's chunk image: CH = 1024 / LPB sample rows of
+// LPB lines x ES bytes, ES wave-instructions of 1 KiB, the wave taking every other one.  Slot j
+// holds sample k0 + dk * j (clamped into the line: the slots past its end are never read).
+template <int LPB, int ES>
+__device__ __forceinline__ void th_issue(const char* g, size_t st, int l0, int k0, int dk, int last, char* img,
+                                         int lw, int lane) {
+    constexpr int SB = LPB * ES;  // bytes of a slot
+    static_assert(ES % 2 == 0 && SB % 16 == 0, "two loader waves, whole pieces");
+#pragma unroll
+    for (int q = 0; q < ES / 2; q++) {
+        const int ii = 2 * q + lw;  // wave-uniform
+        const int off = ii * 1024 + lane * 16;
+        const int j = off / SB, b = off - j * SB;
+        const int k = min(max(k0 + dk * j, 0), last);
+        const char* src = g + ((size_t)k * st + l0) * ES + b;
+        __builtin_amdgcn_global_load_lds((th_glb_ptr)src, (th_lds_ptr)(img + ii * 1024), 16, 0, 0);
+    }
+}
+
+// waits until at most m of the wave's younger chunks (IW instructions each) are in flight
+template <int IW> __device__ __forceinline__ void th_wait_chunks(int m) {
+    static_assert(kThNB == 5, "m <= kThNB - 3");
+    if (m >= 2) th_vmcnt<2 * IW>();
+    else if (m == 1) th_vmcnt<IW>();
+    else th_vmcnt<0>();
+}
+
+// A loader wave over one phase of nch chunks (chunk c = samples k0 + dk * (c * CH + j)): chunks
+// 0 .. kThNB-2 ahead, then per iteration c chunk c + kThNB - 1 into the buffer chunk c - 1 left,
+// and chunk c + 2 landed before the barrier; 1 + nch barriers, as every wave of the phase.
+template <int LPB, int ES0, int ES1>
+__device__ __forceinline__ void th_load_phase(const char* g0, const char* g1, size_t st, int l0, int k0, int dk,
+                                              int last, int nch, char* lds, int lw, int lane) {
+    constexpr int CH = 1024 / LPB, IW = (ES0 + ES1) / 2;
+    auto issue = [&](int c) __attribute__((always_inline)) {
+        char* buf = lds + (c % kThNB) * kThBuf;
+        th_issue<LPB, ES0>(g0, st, l0, k0 + dk * c * CH, dk, last, buf, lw, lane);
+        if constexpr (ES1 > 0) th_issue<LPB, ES1>(g1, st, l0, k0 + dk * c * CH, dk, last, buf + 1024 * ES0, lw, lane);
+    };
+    const int pre = min(kThNB - 1, nch);
+    for (int c = 0; c < pre; c++) issue(c);
+    th_wait_chunks<IW>(pre - 2);
+    th_barrier();
+    for (int c = 0; c < nch; c++) {
+        if (c + kThNB - 1 < nch) issue(c + kThNB - 1);
+        if (lw == 0) TH_STAMP(2, (dk < 0 ? 512 : 0) + c);
+        th_wait_chunks<IW>(min(c + kThNB - 1, nch - 1) - (c + 2));
+        if (lw == 0) TH_STAMP(3, (dk < 0 ? 512 : 0) + c);
+        th_barrier();
+    }
+}
+
+// The writer wave: the solver's rows of chunk c (double-buffered by chunk parity) go to memory
+// during iteration c + 1, the last chunk's after the phase's final barrier.
+//   fwd:  row j = sample c * CH + j of the forward values, k-major in place (a row = the block's
+//         LPB lines, contiguous); all in memory (vmcnt(0)) before the barrier that ends the phase,
+//         since the back substitution's loaders read them
+//   back: row j = sample kb - j, kb = last - 1 - c * CH, in the padded ThRows layout: line-major
+//         into O (a wave-instruction: CH consecutive samples of 64 / CH lines) or k-major split
+//         into O0 / O1 (the last pass)
+//   job:  row j = (a, den, 1/den, t) of sample c * CH + j -> coef and tt, k-major
+template <bool TWO, int LPB>
+__device__ __forceinline__ void th_write_fwd_phase(void* U, size_t st, size_t fofs, int l0, int nl, int last, int nch,
+                                                   const char* orow, int lane) {
+    typedef typename FgsRhs<TWO>::T V;
+    constexpr int ES = TWO ? 8 : 4, CH = 1024 / LPB;
+    const int line = lane % LPB;
+    const bool lv = l0 + line < nl;
+    V* u = (V*)U + fofs + l0 + line;
+    auto put = [&](int c) __attribute__((always_inline)) {
+        const char* rows = orow + (c & 1) * 1024 * ES;
+#pragma unroll 4
+        for (int it = 0; it < 16; it++) {
+            const int jj = it * (64 / LPB) + lane / LPB;
+            const int k = c * CH + jj;
+            if (lv && k <= last) u[(size_t)k * st] = *(const V*)(rows + (jj * LPB + line) * ES);
+        }
+    };
+    th_barrier();
+    for (int c = 0; c < nch; c++) {
+        if (c > 0) put(c - 1);
+        TH_STAMP(4, c);
+        th_barrier();
+    }
+    if (nch > 0) put(nch - 1);
+    th_vmcnt<0>();
+}
+
+template <bool TWO, int LPB>
+__device__ __forceinline__ void th_write_back_phase(const FgsThArgs& a, size_t fofs, int l0, int last, int nch,
+                                                    const char* orow, int lane) {
+    typedef typename FgsRhs<TWO>::T V;
+    constexpr int ES = TWO ? 8 : 4;
+    typedef ThRows<LPB, ES> RW;
+    constexpr int CH = RW::CH;
+    auto put = [&](int c) __attribute__((always_inline)) {
+        const char* rows = orow + (c & 1) * CH * RW::S * 4;
+        const int kb = last - 1 - c * CH;
+        if (a.O) {
+            const int cnt = min(CH, kb + 1), kmin = kb - cnt + 1;
+            const int s = lane % CH;
+#pragma unroll 4
+            for (int it = 0; it < 16; it++) {
+                const int line = it * (64 / CH) + lane / CH;
+                if (s < cnt && l0 + line < a.nl) {
+                    const int k = kmin + s;
+                    const V v = *(const V*)(rows + (kb - k) * RW::S * 4 + line * ES);
+                    ((V*)a.O)[fofs + (size_t)(l0 + line) * a.onp + k] = v;
+                }
+            }
+        } else {
+            const int line = lane % LPB;
+            const size_t fo = (size_t)blockIdx.y * a.ofs + l0 + line;
+#pragma unroll 4
+            for (int it = 0; it < 16; it++) {
+                const int jj = it * (64 / LPB) + lane / LPB;
+                const int k = kb - jj;
+                if (k >= 0 && l0 + line < a.nl) {
+                    const V v = *(const V*)(rows + jj * RW::S * 4 + line * ES);
+                    a.O0[fo + (size_t)k * a.ost] = FgsRhs<TWO>::x(v);
+                    if constexpr (TWO) a.O1[fo + (size_t)k * a.ost] = FgsRhs<TWO>::y(v);
+                }
+            }
+        }
+    };
+    th_barrier();
+    for (int c = 0; c < nch; c++) {
+        if (c > 0) put(c - 1);
+        th_barrier();
+    }
+    if (nch > 0) put(nch - 1);
+}
+
+template <int LPB>
+__device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t fofs, int l0, int nch, const char* orow,
+                                                   int lane) {
+    constexpr int CH = 1024 / LPB;
+    const int line = lane % LPB, last = J.n - 1;
+    const bool lv = l0 + line < J.nl;
+    float4* co = J.coef + fofs + l0 + line;
+    float* tt = J.tt + fofs + l0 + line;
+    const size_t st = (size_t)J.st;
+    auto put = [&](int c) __attribute__((always_inline)) {
+        const char* rows = orow + (c & 1) * 1024 * 16;
+#pragma unroll 4
+        for (int it = 0; it < 16; it++) {
+            const int jj = it * (64 / LPB) + lane / LPB;
+            const int k = c * CH + jj;
+            if (lv && k <= last) {
+                const float4 v = *(const float4*)(rows + (jj * LPB + line) * 16);
+                co[(size_t)k * st] = v;
+                tt[(size_t)k * st] = v.w;
+            }
+        }
+    };
+    th_barrier();
+    for (int c = 0; c < nch; c++) {
+        if (c > 0) put(c - 1);
+        th_barrier();
+    }
+    if (nch > 0) put(nch - 1);
+}
+
+// a coefficient job's LPB lines on the solver wave: the t recurrence; (a, den, 1/den, t) per
+// sample into the writer's rows
+template <int LPB>
+__device__ __forceinline__ void th_job_solver(const FgsCoefJob& J, int l0, int lane, const char* lds, char* orow) {
+    constexpr int CH = 1024 / LPB;
+    const int ln = lane & (LPB - 1);
+    const int last = J.n - 1, nch = (J.n + CH - 1) / CH;
+    const float lam = J.lam;
+    float rc[kThPF];
+    th_barrier();
+#pragma unroll
+    for (int j = 0; j < kThPF; j++) rc[j] = *(const float*)(lds + (j * LPB + ln) * 4);
+    float cprev = 0.0f, tprev = 0.0f;
+    for (int c = 0; c < nch; c++) {
+        const char* cur = lds + (c % kThNB) * kThBuf;
+        const char* nxt = lds + ((c + 1) % kThNB) * kThBuf;
+        const int kc = c * CH;
+        char* w = orow + (c & 1) * 1024 * 16 + ln * 16;
+        auto body = [&](auto guard) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const float cw = rc[j % kThPF];
+                const int jn = j + kThPF;
+                rc[j % kThPF] = jn < CH ? *(const float*)(cur + (jn * LPB + ln) * 4)
+                                        : *(const float*)(nxt + ((jn - CH) * LPB + ln) * 4);
+                if (!decltype(guard)::value || kc + j <= last) {
+                    const float aa = lam * cprev;
+                    const float cc = lam * cw;
+                    const float den = (1.0f - cc) - aa * (1.0f + tprev);
+                    tprev = cc / den;
+                    *(float4*)(w + j * LPB * 16) = make_float4(aa, den, 1.0f / den, tprev);
+                    cprev = cw;
+                }
+            }
+        };
+        if (kc + CH - 1 <= last) body(std::false_type{});
+        else body(std::true_type{});
+        th_lgkm0();
+        th_barrier();
+    }
+}
+
+// The solver wave of one pass: forward elimination (streams U and (a, den, 1/den, t)), then the
+// back substitution (streams U -- the forward values -- and t); every result into the writer's
+// LDS rows.
+template <bool TWO, int LPB>
+__device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, int l0, int lane, const char* lds,
+                                               char* orow) {
+    typedef FgsRhs<TWO> R;
+    typedef typename R::T V;
+    constexpr int ESU = TWO ? 8 : 4;
+    constexpr int CH = 1024 / LPB;
+    constexpr int S1 = 1024 * ESU;  // stream 1's offset in a chunk buffer
+    typedef ThRows<LPB, ESU> RW;
+    const int ln = lane & (LPB - 1);
+    const int l = l0 + ln;
+    const bool valid = lane < LPB && l < a.nl;
+    const int n = a.n, last = n - 1;
+    const int nch = (n + CH - 1) / CH;
+    auto rdu = [&](const char* buf, int j) __attribute__((always_inline)) {
+        return *(const V*)(buf + (j * LPB + ln) * ESU);
+    };
+    auto rdq = [&](const char* buf, int j) __attribute__((always_inline)) {
+        return *(const float4*)(buf + S1 + (j * LPB + ln) * 16);
+    };
     // ---- forward elimination ----
-    float r0[PF], r1[PF], rc[PF];
-#pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const size_t o = (size_t)min(j, last) * st;
-        r0[j] = u0[o];
-        if constexpr (U1) r1[j] = u1[o];
-        rc[j] = cw[o];
-    }
-    float cprev = 0.0f, tprev = 0.0f, p0 = 0.0f, p1 = 0.0f;
-    auto fwd = [&](int k, int j) __attribute__((always_inline)) {
-        const size_t o = (size_t)k * st;
-        const float aa = lam * cprev;
-        const float c = lam * rc[j];
-        const float den = (1.0f - c) - aa * (1.0f + tprev);
-        tprev = c / den;
-        p0 = (r0[j] - aa * p0) / den;
-        if constexpr (U1) p1 = (r1[j] - aa * p1) / den;
-        cprev = rc[j];
-        t[o] = tprev;
-        u0[o] = p0;
-        if constexpr (U1) u1[o] = p1;
+    V ru[kThPF];
+    float4 rq[kThPF];
+    auto rd = [&](const char* buf, int j, int r) __attribute__((always_inline)) {
+        ru[r] = rdu(buf, j);
+        rq[r] = rdq(buf, j);
     };
-    int k0 = 0;
-    for (;; k0 += PF) {
-        float n0[PF], n1[PF], nc[PF];
+    th_barrier();
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const size_t o = (size_t)min(k0 + PF + j, last) * st;
-            n0[j] = u0[o];
-            if constexpr (U1) n1[j] = u1[o];
-            nc[j] = cw[o];
+    for (int j = 0; j < kThPF; j++) rd(lds, j, j);
+    float p0 = 0.0f, p1 = 0.0f;
+    for (int c = 0; c < nch; c++) {
+        const char* cur = lds + (c % kThNB) * kThBuf;
+        const char* nxt = lds + ((c + 1) % kThNB) * kThBuf;
+        const int kc = c * CH;
+        char* wu = orow + (c & 1) * 1024 * ESU + ln * ESU;  // this chunk's rows
+        TH_STAMP(0, c);
+        const float ps0 = p0, ps1 = p1;
+        uint32_t key = 0xffffffffu;
+        auto body = [&](auto guard) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const int r = j % kThPF;
+                const V xu = ru[r];
+                const float4 xq = rq[r];  // a, den, 1/den, t
+                const int jn = j + kThPF;
+                if (jn < CH) rd(cur, jn, r);
+                else rd(nxt, jn - CH, r);
+                if (!decltype(guard)::value || kc + j <= last) {
+#ifdef SDR_TH_EXP_NOCHAIN
+                    p0 = R::x(xu) + xq.x;
+                    p1 = R::y(xu) + xq.y;
+                    if (false) {
+#else
+                    {
+#endif
+                    const float x0 = R::x(xu) - xq.x * p0;
+                    const float q00 = x0 * xq.z;
+                    p0 = __builtin_fmaf(-__builtin_fmaf(q00, xq.y, -x0), xq.z, q00);
+                    uint32_t kk = fgs_tiny_key(q00);
+                    if constexpr (TWO) {
+                        const float x1 = R::y(xu) - xq.x * p1;
+                        const float q01 = x1 * xq.z;
+                        p1 = __builtin_fmaf(-__builtin_fmaf(q01, xq.y, -x1), xq.z, q01);
+                        kk = min(kk, fgs_tiny_key(q01));
+                    }
+                    key = min(key, kk);
+                    }
+#ifdef SDR_TH_EXP_MASKW
+                    if (lane < LPB)
+#endif
+                    *(V*)(wu + j * LPB * ESU) = R::make(p0, p1);
+                }
+            }
+        };
+        if (kc + CH - 1 <= last) body(std::false_type{});
+        else body(std::true_type{});
+        // a chunk with a quotient the reciprocal form does not cover (rare: right-hand sides
+        // decayed below 2^-96) runs again from its start with real divisions, its rows
+        // overwriting the first run's (the chunk's buffer is intact until the barrier)
+        if (__builtin_amdgcn_ballot_w64(valid && key < kFgsTinyKey)) {
+            p0 = ps0;
+            p1 = ps1;
+            for (int j = 0; j < CH && kc + j <= last; j++) {
+                const V xu = rdu(cur, j);
+                const float4 xq = rdq(cur, j);
+                p0 = (R::x(xu) - xq.x * p0) / xq.y;
+                if constexpr (TWO) p1 = (R::y(xu) - xq.x * p1) / xq.y;
+                *(V*)(wu + j * LPB * ESU) = R::make(p0, p1);
+            }
         }
-        if (k0 + PF - 1 <= last) {
-#pragma unroll
-            for (int j = 0; j < PF; j++) fwd(k0 + j, j);
-        } else {
-#pragma unroll
-            for (int j = 0; j < PF; j++)
-                if (k0 + j <= last) fwd(k0 + j, j);
-        }
-        if (k0 + PF > last) break;
-        // whole-array copies (register renames after SROA; an element loop here was rewritten
-        // into a copy idiom before the unroller ran, which then warned)
-        __builtin_memcpy(r0, n0, sizeof r0);
-        if constexpr (U1) __builtin_memcpy(r1, n1, sizeof r1);
-        __builtin_memcpy(rc, nc, sizeof rc);
+        TH_STAMP(1, c);
+        th_lgkm0();
+        th_barrier();
     }
+    // (the writer has the forward values in memory before this barrier)
+    th_barrier();
     // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
-    if (last < 1) return;
-    float q0 = p0, q1 = p1;
-    float b0[PF], b1[PF], bt[PF];
-#pragma unroll
-    for (int j = 0; j < PF; j++) {
-        const size_t o = (size_t)max(last - 1 - j, 0) * st;
-        b0[j] = u0[o];
-        if constexpr (U1) b1[j] = u1[o];
-        bt[j] = t[o];
+    if (valid) {
+        if (a.O) ((V*)a.O)[fofs + (size_t)l * a.onp + last] = R::make(p0, p1);
+        else {
+            a.O0[(size_t)blockIdx.y * a.ofs + (size_t)last * a.ost + l] = p0;
+            if constexpr (TWO) a.O1[(size_t)blockIdx.y * a.ofs + (size_t)last * a.ost + l] = p1;
+        }
     }
-    auto bwd = [&](int k, int j) __attribute__((always_inline)) {
-        const size_t o = (size_t)k * st;
-        q0 = b0[j] - bt[j] * q0;
-        u0[o] = q0;
-        if constexpr (U1) {
-            q1 = b1[j] - bt[j] * q1;
-            u1[o] = q1;
-        }
+    const int nchb = (last + CH - 1) / CH;
+    float q0 = p0, q1 = p1;
+    V bu[kThPF];
+    float bt[kThPF];
+    auto rdb = [&](const char* buf, int j, int r) __attribute__((always_inline)) {
+        bu[r] = rdu(buf, j);
+        bt[r] = *(const float*)(buf + S1 + (j * LPB + ln) * 4);
     };
-    for (int k1 = last - 1;; k1 -= PF) {
-        float n0[PF], n1[PF], nt[PF];
+    th_barrier();
 #pragma unroll
-        for (int j = 0; j < PF; j++) {
-            const size_t o = (size_t)max(k1 - PF - j, 0) * st;
-            n0[j] = u0[o];
-            if constexpr (U1) n1[j] = u1[o];
-            nt[j] = t[o];
+    for (int j = 0; j < kThPF; j++) rdb(lds, j, j);
+    for (int c = 0; c < nchb; c++) {
+        const char* cur = lds + (c % kThNB) * kThBuf;
+        const char* nxt = lds + ((c + 1) % kThNB) * kThBuf;
+        char* rows = orow + (c & 1) * CH * RW::S * 4 + ln * ESU;
+        const int kb = last - 1 - c * CH;
+        TH_STAMP(0, 512 + c);
+        auto body = [&](auto guard) __attribute__((always_inline)) {
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const int r = j % kThPF;
+                const V xu = bu[r];
+                const float xt = bt[r];
+                const int jn = j + kThPF;
+                if (jn < CH) rdb(cur, jn, r);
+                else rdb(nxt, jn - CH, r);
+                if (!decltype(guard)::value || kb - j >= 0) {
+                    q0 = R::x(xu) - xt * q0;
+                    if constexpr (TWO) q1 = R::y(xu) - xt * q1;
+#ifdef SDR_TH_EXP_MASKW
+                    if (lane < LPB)
+#endif
+                    *(V*)(rows + j * RW::S * 4) = R::make(q0, q1);
+                }
+            }
+        };
+        if (kb - CH + 1 >= 0) body(std::false_type{});
+        else body(std::true_type{});
+        TH_STAMP(1, 512 + c);
+        th_lgkm0();
+        th_barrier();
+    }
+}
+
+// One FGS pass (all lines of F frames) in ximgproc's order from its jobs' coefficients; blocks
+// past main_blocks run coefficient jobs (a.job) instead (a launch of jobs alone: main_blocks = 0).
+// 256 threads: solver, two loaders, writer.
+template <bool TWO, int LPB>
+__global__ __launch_bounds__(256) void k_fgs_th(FgsThArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[kThLds];
+    char* orow = lds + kThNB * kThBuf;
+    constexpr int CH = 1024 / LPB;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const size_t fofs = (size_t)blockIdx.y * a.fs;
+    const int blk = blockIdx.x;
+    if (blk >= a.main_blocks) {
+        int jb = blk - a.main_blocks, j = 0;
+        while (j < a.njobs && jb >= a.job[j].blocks) jb -= a.job[j++].blocks;
+        if (j >= a.njobs) return;  // uniform over the workgroup
+        const FgsCoefJob& J = a.job[j];
+        const int l0 = jb * LPB, nch = (J.n + CH - 1) / CH;
+        if (wave == 0) th_job_solver<LPB>(J, l0, lane, lds, orow);
+        else if (wave <= 2)
+            th_load_phase<LPB, 4, 0>((const char*)(J.Cw + fofs), nullptr, J.st, l0, 0, 1, J.n - 1, nch, lds,
+                                     wave - 1, lane);
+        else th_write_job_phase<LPB>(J, fofs, l0, nch, orow, lane);
+        return;
+    }
+    constexpr int ESU = TWO ? 8 : 4;
+    const int l0 = blk * LPB, n = a.n, last = n - 1;
+    const int nch = (n + CH - 1) / CH, nchb = (last + CH - 1) / CH;
+    const char* gu = (const char*)a.U + fofs * ESU;
+    if (wave == 0) {
+        th_pass_solver<TWO, LPB>(a, fofs, l0, lane, lds, orow);
+    } else if (wave <= 2) {
+        const int lw = wave - 1;
+        th_load_phase<LPB, ESU, 16>(gu, (const char*)(a.coef + fofs), a.st, l0, 0, 1, last, nch, lds, lw, lane);
+        th_barrier();
+        th_load_phase<LPB, ESU, 4>(gu, (const char*)(a.tt + fofs), a.st, l0, last - 1, -1, last, nchb, lds, lw, lane);
+    } else {
+        th_write_fwd_phase<TWO, LPB>(a.U, a.st, fofs, l0, a.nl, last, nch, orow, lane);
+        th_barrier();
+        th_write_back_phase<TWO, LPB>(a, fofs, l0, last, nchb, orow, lane);
+    }
+}
+
+// R0 (and R1) row-major [h][w] -> the first row pass's input: transposed [w][hp] (hp = h rounded
+// up to 4, frames fgs_pad4(w) * hp apart), the two images interleaved (float2) when R1 is given;
+// 64x64 LDS tiles
+__global__ __launch_bounds__(256) void k_fgs_pack(const float* __restrict__ r0, const float* __restrict__ r1,
+                                                  float* __restrict__ dst, int h, int w) {
+    __shared__ float tile[2][64][65];
+    const int c0 = blockIdx.x * 64, rw0 = blockIdx.y * 64;
+    const size_t fo = (size_t)blockIdx.z * h * w;
+    const int hp = fgs_pad4(h);
+    const size_t fd = (size_t)blockIdx.z * fgs_pad4(w) * hp;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int rr = rw0 + r, cc = c0 + tx;
+        if (rr < h && cc < w) {
+            tile[0][r][tx] = r0[fo + (size_t)rr * w + cc];
+            if (r1) tile[1][r][tx] = r1[fo + (size_t)rr * w + cc];
         }
-        if (k1 - PF + 1 >= 0) {
-#pragma unroll
-            for (int j = 0; j < PF; j++) bwd(k1 - j, j);
-        } else {
-#pragma unroll
-            for (int j = 0; j < PF; j++)
-                if (k1 - j >= 0) bwd(k1 - j, j);
-        }
-        if (k1 - PF < 0) break;
-#pragma unroll
-        for (int j = 0; j < PF; j++) {
-            b0[j] = n0[j];
-            if constexpr (U1) b1[j] = n1[j];
-            bt[j] = nt[j];
+    }
+    __syncthreads();
+    for (int c = ty; c < 64; c += 4) {
+        const int cc = c0 + c, rr = rw0 + tx;
+        if (rr < h && cc < w) {
+            const size_t o = fd + (size_t)cc * hp + rr;
+            if (r1) ((float2*)dst)[o] = make_float2(tile[0][tx][c], tile[1][tx][c]);
+            else dst[o] = tile[0][tx][c];
         }
     }
 }
@@ -466,7 +907,9 @@ __global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__
     const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (j >= w || i >= h) return;
     const uint8_t* g = guide + (size_t)blockIdx.z * gfstride + (size_t)i * gstride + j;
-    const size_t fo = (size_t)blockIdx.z * w * h;
+    // the sequential solver's layouts: Ch at j*hp + i, Cv at i*wp + j (fgs_pad4)
+    const int wp = ch_rowmajor ? w : fgs_pad4(w), hp = ch_rowmajor ? h : fgs_pad4(h);
+    const size_t fo = (size_t)blockIdx.z * wp * hp;
     const int v = g[0];
     float ch = 0.0f, cv = 0.0f;
     if (j + 1 < w) {
@@ -477,8 +920,8 @@ __global__ __launch_bounds__(256) void k_fgs_weights(const uint8_t* __restrict__
         const int d = v - g[gstride];
         cv = lut[d * d];
     }
-    ChT[fo + (ch_rowmajor ? (size_t)i * w + j : (size_t)j * h + i)] = ch;
-    Cv[fo + (size_t)i * w + j] = cv;
+    ChT[fo + (ch_rowmajor ? (size_t)i * w + j : (size_t)j * hp + i)] = ch;
+    Cv[fo + (size_t)i * wp + j] = cv;
 }
 
 // dst[f][c][r] = src[f][r][c] for two arrays (rows x cols per frame), 64x64 LDS tiles
@@ -624,13 +1067,22 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
         const float conf = 255.0f * c;
         if (conf_full) conf_full[fo + o] = conf;
         if (in_roi) {
-            A[cf + j] = conf * (float)v;
-            B[cf + j] = conf;
+            if (ch_rowmajor) {
+                A[cf + j] = conf * (float)v;
+                B[cf + j] = conf;
+            } else {
+                // the sequential solver's first pass reads them transposed ([column][row]), the two
+                // right-hand sides interleaved (A is its pass buffer, B unused)
+                ((float2*)A)[(size_t)f * fgs_pad4(rw) * fgs_pad4(g.rh) + (size_t)j * fgs_pad4(g.rh) + i] =
+                    make_float2(conf * (float)v, conf);
+            }
         }
     }
     // FGS weights of the guide's ROI row i (k_fgs_weights' formulas)
     const uint8_t* gr = guide + (size_t)f * gfstride + (size_t)(g.ry + i) * gstride + g.rx;
-    const size_t wfo = (size_t)f * rw * g.rh;
+    // (the sequential solver's layouts: Ch at j*hp + i, Cv at i*wp + j; fgs_pad4)
+    const int wp = ch_rowmajor ? rw : fgs_pad4(rw), hp = ch_rowmajor ? g.rh : fgs_pad4(g.rh);
+    const size_t wfo = (size_t)f * wp * hp;
     for (int j = tid; j < rw; j += T) {
         const int v = gr[j];
         float ch = 0.0f, cv = 0.0f;
@@ -642,8 +1094,8 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
             const int d = v - gr[gstride + j];
             cv = lut[d * d];
         }
-        ChW[wfo + (ch_rowmajor ? (size_t)i * rw + j : (size_t)j * g.rh + i)] = ch;
-        Cv[wfo + (size_t)i * rw + j] = cv;
+        ChW[wfo + (ch_rowmajor ? (size_t)i * rw + j : (size_t)j * hp + i)] = ch;
+        Cv[wfo + (size_t)i * wp + j] = cv;
     }
 }
 
@@ -667,16 +1119,61 @@ __global__ __launch_bounds__(256) void k_wls_final(const float* __restrict__ A,
 }
 
 // FastGlobalSmootherFilter::filter on nimg (1 or 2) row-major w x h images per frame (R0, R1, in
-// place), F frames sharing per-frame guides.  Scratch (each F*w*h floats): A, B (column-major
-// copies), T (elimination coefficients), ChT, Cv (weights).
+// place), F frames sharing per-frame guides.  Scratch, in frames of fsp = fgs_pad4(w) *
+// fgs_pad4(h) samples (SDR_FGS_PCR uses ChT and Cv only, w * h a frame):
 struct FgsScratch {
-    float *A, *B, *T, *ChT, *Cv;
+    float *A, *B;    // the sequential solver's two pass layouts (2 floats a sample), F frames each
+    float *ChT, *Cv; // the weights, F frames each
+    float* coef;     // the sequential solver's coefficients of each of the 2 * iters passes:
+                     // [F * fsp] float4 (a, den, 1/den, t) then [F * fsp] t (5 * F * fsp floats)
 };
 
-static void fgs_sweep(dim3 grid, hipStream_t st, float* U0, float* U1, const float* Cw, float* T,
-                      int nlines, int n, size_t fs, float lam) {
-    if (U1) hipLaunchKernelGGL((k_fgs_sweep<true>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
-    else hipLaunchKernelGGL((k_fgs_sweep<false>), grid, dim3(64), 0, st, U0, U1, Cw, T, nlines, n, fs, lam);
+#ifdef SDR_TH_STAMPS
+static unsigned long long* th_stamp_buf = nullptr;
+#endif
+
+template <int LPB>
+static void launch_fgs_th_lpb(const dim3& grid, const FgsThArgs& a, bool two, hipStream_t st) {
+    if (two) hipLaunchKernelGGL((k_fgs_th<true, LPB>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_fgs_th<false, LPB>), grid, dim3(256), 0, st, a);
+}
+
+// One k_fgs_th launch: the pass (a.nl lines; none when !pass) or its jobs, with the fewest lines
+// a workgroup (LPB) whose workgroups still all fit on the chip at once (one a CU: the LDS ring),
+// so that every chain runs on a CU's memory pipeline shared with as few lines as possible.
+static void launch_fgs_th(FgsThArgs a, bool pass, bool two, int F, hipStream_t st) {
+    const int cus = device_cus();
+    int lpb = 64;
+#ifdef SDR_TH_FORCE_LPB
+    for (int c : {SDR_TH_FORCE_LPB}) {
+#else
+    for (int c : {16, 32, 64}) {
+#endif
+        int blocks = pass ? (a.nl + c - 1) / c : 0;
+        for (int j = 0; j < a.njobs; j++) blocks += (a.job[j].nl + c - 1) / c;
+        if ((long long)blocks * F <= cus) {
+            lpb = c;
+            break;
+        }
+    }
+    a.main_blocks = pass ? (a.nl + lpb - 1) / lpb : 0;
+    int blocks = a.main_blocks;
+    for (int j = 0; j < a.njobs; j++) blocks += a.job[j].blocks = (a.job[j].nl + lpb - 1) / lpb;
+    const dim3 grid(blocks, F);
+#ifdef SDR_TH_STAMPS
+    {
+        static int launches = 0;
+        static unsigned long long* buf = nullptr;
+        static const int want = getenv("SDR_TH_STAMP_LAUNCH") ? atoi(getenv("SDR_TH_STAMP_LAUNCH")) : -1;
+        if (!buf) (void)hipMalloc((void**)&buf, 5 * 1024 * 8);
+        unsigned long long* v = launches++ == want ? buf : nullptr;
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_th_stamps), &v, sizeof(v), 0, hipMemcpyHostToDevice, st);
+        th_stamp_buf = buf;
+    }
+#endif
+    if (lpb == 16) launch_fgs_th_lpb<16>(grid, a, two, st);
+    else if (lpb == 32) launch_fgs_th_lpb<32>(grid, a, two, st);
+    else launch_fgs_th_lpb<64>(grid, a, two, st);
 }
 
 // k_fgs_pcr instance for G*n samples per block: one equation per thread up to 1024 samples
@@ -722,54 +1219,104 @@ static int launch_pcr(float* U0, float* U1, const float* Cw, int w, int h, int F
 
 // FastGlobalSmootherFilter::filter on R0 (and R1 when non-null: a second right-hand side of the
 // same systems), row-major w x h per frame, F frames with per-frame guides, in place.
+//   SDR_FGS_THOMAS: weights (ChT column-major = the row pass's k-major, Cv row-major = the column
+//                   pass's), the right-hand sides transposed into s.A (in_transposed: the caller
+//                   already wrote them there), one launch of coefficient jobs (every pass's
+//                   (a, den, 1/den, t)), then the passes of k_fgs_th alternating between the two
+//                   layouts (row pass: s.A -> s.B, column pass: s.B -> s.A; the last column pass
+//                   into R0 / R1): 2 * iters + 1 launches
 //   SDR_FGS_PCR:    weights (Ch, Cv row-major), then per iteration k_fgs_pcr over the rows and
 //                   over the columns of the images themselves (2 launches per iteration)
-//   SDR_FGS_THOMAS: weights (ChT column-major, Cv), then per iteration transpose -> row sweep ->
-//                   transpose back -> column sweep (4 launches per iteration)
-// Scratch (each F*w*h floats): A, B (column-major copies, THOMAS), T (THOMAS), ChT, Cv (weights).
 static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, const float* lut,
                       float* R0, float* R1, int w, int h, int F, double lambda, double att,
                       int iters, int solver, const FgsScratch& s, hipStream_t st,
                       bool weights_ready = false, sdr_sgbm* timer = nullptr,
-                      const WlsGeom* fin_g = nullptr, const WlsOut* fin_o = nullptr) {
+                      const WlsGeom* fin_g = nullptr, const WlsOut* fin_o = nullptr,
+                      bool in_transposed = false) {
     const size_t fs = (size_t)w * h;
     const bool pcr = solver == SDR_FGS_PCR;
     if (!weights_ready)
         hipLaunchKernelGGL(k_fgs_weights, dim3((w + 63) / 64, (h + 3) / 4, F), dim3(256), 0, st, guide,
                            gstride, gfstride, lut, w, h, pcr ? 1 : 0, s.ChT, s.Cv);
-    const dim3 t_rm((w + 63) / 64, (h + 63) / 64, F), t_cm((h + 63) / 64, (w + 63) / 64, F);
     float lam = (float)lambda;
     const float fa = (float)att;
-    for (int it = 0; it < iters; it++) {
-        if (pcr) {
-            int e1, e2;
-            {
-                KScope kt(timer, SDR_KERNEL_FGS);
-                e1 = R1 ? launch_pcr<true>(R0, R1, s.ChT, w, h, F, 1, lam, st)
-                        : launch_pcr<false>(R0, R1, s.ChT, w, h, F, 1, lam, st);
+    if (!pcr) {
+        if (iters <= 0) return 0;
+        const bool two = R1 != nullptr;
+        if (!in_transposed)
+            hipLaunchKernelGGL(k_fgs_pack, dim3((w + 63) / 64, (h + 63) / 64, F), dim3(256), 0, st, R0, R1, s.A, h, w);
+        const int npass = 2 * iters;
+        // pass p: iteration p / 2, rows (even p: lines = rows, k = column) or columns (odd p);
+        // k-major arrays with sample rows of fgs_pad4(lines)
+        const int wp = fgs_pad4(w), hp = fgs_pad4(h);
+        const size_t fsp = (size_t)wp * hp;
+        std::vector<float> lams(iters);
+        for (int it = 0; it < iters; it++, lam = lam * fa) lams[it] = lam;  // lambda *= attenuation
+        auto pass_args = [&](int p) {
+            FgsThArgs a{};
+            const bool rows = (p & 1) == 0;
+            a.nl = rows ? h : w;
+            a.n = rows ? w : h;
+            a.st = rows ? hp : wp;
+            a.onp = rows ? wp : hp;
+            a.fs = fsp;
+            a.ost = (size_t)w;
+            a.ofs = fs;
+            // rows: transposed (s.A) -> row-major (s.B); columns: row-major (s.B) -> transposed (s.A),
+            // the last pass split back into R0 / R1
+            a.U = rows ? s.A : s.B;
+            const bool last = p == npass - 1;
+            a.O = last ? nullptr : rows ? s.B : s.A;
+            a.O0 = last ? R0 : nullptr;
+            a.O1 = last ? R1 : nullptr;
+            // the pass's coefficient block: float4 (a, den, 1/den, t), then t alone
+            float* cb = s.coef + (size_t)p * 5 * F * fsp;
+            a.coef = (const float4*)cb;
+            a.tt = cb + 4 * F * fsp;
+            return a;
+        };
+        // the coefficient jobs of every pass (kFgsMaxJobs a launch), then the passes
+        for (int p0 = 0; p0 < npass; p0 += kFgsMaxJobs) {
+            FgsThArgs c{};
+            c.fs = fsp;
+            for (int p = p0; p < npass && c.njobs < kFgsMaxJobs; p++) {
+                const FgsThArgs q = pass_args(p);
+                const bool rows = (p & 1) == 0;
+                FgsCoefJob& j = c.job[c.njobs++];
+                j.Cw = rows ? s.ChT : s.Cv;
+                j.coef = (float4*)q.coef;
+                j.tt = (float*)q.tt;
+                j.lam = lams[p / 2];
+                j.nl = q.nl;
+                j.n = q.n;
+                j.st = q.st;
             }
-            {
-                KScope kt(timer, SDR_KERNEL_FGS);
-                // the last column pass writes the filter's outputs itself (fin_g / fin_o)
-                if (fin_g && R1 && it == iters - 1)
-                    e2 = launch_pcr<true, true>(R0, R1, s.Cv, w, h, F, 0, lam, st, *fin_g, *fin_o);
-                else
-                    e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
-                            : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
-            }
-            if (e1 || e2) return -1;
-        } else {
-            {
-                // row pass on column-major copies (lines = rows, k = column)
-                KScope kt(timer, SDR_KERNEL_FGS);
-                hipLaunchKernelGGL(k_transpose2, t_rm, dim3(256), 0, st, R0, R1, s.A, R1 ? s.B : nullptr, h, w);
-                fgs_sweep(dim3((h + 63) / 64, F), st, s.A, R1 ? s.B : nullptr, s.ChT, s.T, h, w, fs, lam);
-                hipLaunchKernelGGL(k_transpose2, t_cm, dim3(256), 0, st, s.A, R1 ? s.B : nullptr, R0, R1, w, h);
-            }
-            // column pass in place on the row-major images (lines = columns, k = row)
-            KScope kt(timer, SDR_KERNEL_FGS);
-            fgs_sweep(dim3((w + 63) / 64, F), st, R0, R1, s.Cv, s.T, w, h, fs, lam);
+            KScope kt(timer, SDR_KERNEL_FGS_COEF);
+            launch_fgs_th(c, false, two, F, st);
         }
+        for (int p = 0; p < npass; p++) {
+            KScope kt(timer, SDR_KERNEL_FGS);
+            launch_fgs_th(pass_args(p), true, two, F, st);
+        }
+        return 0;
+    }
+    for (int it = 0; it < iters; it++) {
+        int e1, e2;
+        {
+            KScope kt(timer, SDR_KERNEL_FGS);
+            e1 = R1 ? launch_pcr<true>(R0, R1, s.ChT, w, h, F, 1, lam, st)
+                    : launch_pcr<false>(R0, R1, s.ChT, w, h, F, 1, lam, st);
+        }
+        {
+            KScope kt(timer, SDR_KERNEL_FGS);
+            // the last column pass writes the filter's outputs itself (fin_g / fin_o)
+            if (fin_g && R1 && it == iters - 1)
+                e2 = launch_pcr<true, true>(R0, R1, s.Cv, w, h, F, 0, lam, st, *fin_g, *fin_o);
+            else
+                e2 = R1 ? launch_pcr<true>(R0, R1, s.Cv, w, h, F, 0, lam, st)
+                        : launch_pcr<false>(R0, R1, s.Cv, w, h, F, 0, lam, st);
+        }
+        if (e1 || e2) return -1;
         lam = lam * fa;  // FastGlobalSmootherFilterImpl::filter: lambda *= lambda_attenuation
     }
     return 0;
@@ -792,7 +1339,7 @@ struct sdr_wls {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t own_stream = nullptr;
-    sdr::Buf rdisc, conf, A, B, Ac, Bc, T, ChT, Cv, lut, out, hbuf;
+    sdr::Buf rdisc, conf, A, B, Ac, Bc, ChT, Cv, lut, out, hbuf, coef;
     double lut_sigma = -1.0;
 };
 
@@ -854,7 +1401,7 @@ void sdr_wls_params_for_sgbm(sdr_sgbm_params* m, sdr_wls_params* p) {
     p->top_offset = 0;
     p->bottom_offset = 0;
     p->min_disp = m->minDisparity;
-    p->fgs_solver = SDR_FGS_PCR;
+    p->fgs_solver = SDR_FGS_THOMAS;  // ximgproc's own elimination order (sdr.h)
 }
 
 int sdr_wls_create(const sdr_wls_params* p, int device, sdr_wls** out) {
@@ -878,8 +1425,8 @@ int sdr_wls_destroy(sdr_wls* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (sdr::Buf* b : {&h->rdisc, &h->conf, &h->A, &h->B, &h->Ac, &h->Bc, &h->T, &h->ChT, &h->Cv,
-                        &h->lut, &h->out, &h->hbuf})
+    for (sdr::Buf* b : {&h->rdisc, &h->conf, &h->A, &h->B, &h->Ac, &h->Bc, &h->ChT, &h->Cv,
+                        &h->lut, &h->out, &h->hbuf, &h->coef})
         if (b->p) (void)hipFree(b->p);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     delete h;
@@ -964,16 +1511,30 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     int rc;
     const float* lut = nullptr;
     if (!fused && (rc = sdr::ensure(h->rdisc, F * px * 4))) return rc;
-    for (sdr::Buf* b : {&h->A, &h->B, &h->ChT, &h->Cv})
+    // the sequential solver's k-major arrays: sample rows padded to 4 lines (fgs_pad4), and room
+    // for its loaders' reads past the last row (kFgsOverread)
+    const size_t cpp = roi ? (size_t)sdr::fgs_pad4(g.rw) * sdr::fgs_pad4(g.rh) : 0;
+    const size_t ov = sdr::kFgsOverread;
+    for (sdr::Buf* b : {&h->A, &h->B})
         if ((rc = sdr::ensure(*b, F * cpx * 4 + 4))) return rc;
-    if (p.fgs_solver == SDR_FGS_THOMAS)
-        for (sdr::Buf* b : {&h->Ac, &h->Bc, &h->T})
-            if ((rc = sdr::ensure(*b, F * cpx * 4 + 4))) return rc;
+    for (sdr::Buf* b : {&h->ChT, &h->Cv})
+        if ((rc = sdr::ensure(*b, F * cpp * 4 + ov))) return rc;
+    if (p.fgs_solver == SDR_FGS_THOMAS) {
+        // the two pass layouts (both right-hand sides interleaved) and every pass's elimination
+        // coefficients (float4 (a, den, 1/den, t) and t: 20 bytes a sample and pass)
+        for (sdr::Buf* b : {&h->Ac, &h->Bc})
+            if ((rc = sdr::ensure(*b, F * cpp * 8 + ov))) return rc;
+        if ((rc = sdr::ensure(h->coef, (size_t)std::max(2 * p.num_iter, 0) * F * cpp * 20 + ov))) return rc;
+    }
     if ((rc = upload_lut(h, p.sigma_color, &lut))) return rc;
     float* A = (float*)h->A.p;
     float* B = (float*)h->B.p;
     const dim3 blk(256);
     const bool rowmajor = p.fgs_solver == SDR_FGS_PCR;
+    // the sequential solver's first pass (rows) reads the right-hand sides transposed: the fused
+    // front end writes them there directly
+    float* Ain = rowmajor ? A : (float*)h->Ac.p;
+    float* Bin = rowmajor ? B : nullptr;
     const dim3 grid((W + 63) / 64, (H + 3) / 4, F);
     sdr::WlsOut wo{out, fout, xyz, {}};
     if (Q)
@@ -987,11 +1548,11 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
         // (setDepthDiscontinuityRadius) take the per-pixel kernels below
         if (g.radius <= 4)
             hipLaunchKernelGGL(sdr::k_wls_prep<4>, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
-                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
+                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, Ain, Bin, (float*)h->ChT.p,
                                (float*)h->Cv.p, fin_fused ? 1 : 0, wo);
         else
             hipLaunchKernelGGL(sdr::k_wls_prep<9>, dim3(H, F), blk, (size_t)g.rw * 32, st, dl, dr, g, guide,
-                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, A, B, (float*)h->ChT.p,
+                               gstride, gfstride, lut, rowmajor ? 1 : 0, conf, Ain, Bin, (float*)h->ChT.p,
                                (float*)h->Cv.p, fin_fused ? 1 : 0, wo);
     } else {
         sdr::KScope kt(timer, SDR_KERNEL_WLS_PREP);
@@ -1003,11 +1564,11 @@ int sdr::wls_filter_enqueue(sdr_wls* h, const int16_t* dl, const int16_t* dr, co
     }
     if (roi) {
         const uint8_t* g0 = guide + (size_t)g.ry * gstride + g.rx;
-        const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->T.p, (float*)h->ChT.p,
-                                 (float*)h->Cv.p};
+        const sdr::FgsScratch fs{(float*)h->Ac.p, (float*)h->Bc.p, (float*)h->ChT.p,
+                                 (float*)h->Cv.p, (float*)h->coef.p};
         if (sdr::launch_fgs(g0, gstride, gfstride, lut, A, B, g.rw, g.rh, F, p.lambda,
                             p.lambda_attenuation, p.num_iter, p.fgs_solver, fs, st, fused, timer,
-                            fin_fused ? &g : nullptr, fin_fused ? &wo : nullptr))
+                            fin_fused ? &g : nullptr, fin_fused ? &wo : nullptr, fused && !rowmajor))
             return sdr::set_error(SDR_ERR_SIZE, "SDR_FGS_PCR solves lines of at most 4096 samples "
                                                 "(use SDR_FGS_THOMAS for larger ROIs)");
         if (fin_fused) {
@@ -1059,6 +1620,14 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8
     return SDR_OK;
 }
 
+#ifdef SDR_TH_STAMPS
+// diagnostic build only: the stamps of the launch SDR_TH_STAMP_LAUNCH names ([5][1024] u64)
+int sdr_th_stamps(unsigned long long* host) {
+    if (!sdr::th_stamp_buf) return -1;
+    return hipMemcpy(host, sdr::th_stamp_buf, 5 * 1024 * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, double lambda,
                           double sigma, double att, int iters, float* d_img, int nimg,
                           int solver, void* stream) {
@@ -1079,10 +1648,16 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
     float* dlut = nullptr;
     float* scr = nullptr;
     const size_t px = (size_t)w * h;
+    // (frames of the sequential solver's padded layouts: fgs_pad4(w) * fgs_pad4(h) >= px samples)
+    const size_t fp = (size_t)sdr::fgs_pad4(w) * sdr::fgs_pad4(h);
     WLS_HIP(hipMallocAsync((void**)&dlut, sizeof(float) * lut.size(), st));
-    WLS_HIP(hipMallocAsync((void**)&scr, sizeof(float) * px * 5, st));
+    // (FgsScratch: the sequential solver's two interleaved pass layouts, the weights, and 5 floats
+    // a sample for each of its 2 * iters passes' coefficients; its loaders read up to
+    // kFgsOverread bytes past an array)
+    const size_t ncoef = solver == SDR_FGS_THOMAS ? (size_t)5 * (2 * iters) : 0;
+    WLS_HIP(hipMallocAsync((void**)&scr, sizeof(float) * fp * (6 + ncoef) + sdr::kFgsOverread, st));
     WLS_HIP(hipMemcpyAsync(dlut, lut.data(), sizeof(float) * lut.size(), hipMemcpyHostToDevice, st));
-    const sdr::FgsScratch fs{scr, scr + px, scr + 2 * px, scr + 3 * px, scr + 4 * px};
+    const sdr::FgsScratch fs{scr, scr + 2 * fp, scr + 4 * fp, scr + 5 * fp, scr + 6 * fp};
     // images are filtered in pairs (two right-hand sides of one system per line)
     for (int i = 0; i < nimg; i += 2) {
         const int m = nimg - i >= 2 ? 2 : 1;

@@ -33,7 +33,7 @@ UNIQ_AUTO, UNIQ_SCALAR, UNIQ_SIMD = 0, 1, 2
 # SDR_KERNEL_* (include/sdr/sdr.h)
 (KERNEL_PREFILTER, KERNEL_COST, KERNEL_PATHS, KERNEL_WTA_LR, KERNEL_MEDIAN, KERNEL_SPECKLE,
  KERNEL_REPROJECT, KERNEL_LR_CHECK, KERNEL_SWEEP, KERNEL_WLS_PREP, KERNEL_FGS, KERNEL_WLS_FINAL,
- KERNEL_SWEEP_DOWN) = range(13)
+ KERNEL_SWEEP_DOWN, KERNEL_FGS_COEF) = range(14)
 DEBUG_SWEEP_SPIN = 1  # sdr_sgbm_debug_knob
 
 

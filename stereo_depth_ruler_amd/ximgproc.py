@@ -55,7 +55,7 @@ class DisparityWLSFilter:
     def setLRCthresh(self, v): self._set("lrc_thresh", int(v))
     def getDepthDiscontinuityRadius(self): return self._p.depth_discontinuity_radius
     def setDepthDiscontinuityRadius(self, v): self._set("depth_discontinuity_radius", int(v))
-    # engine extension: the FGS line solver (FGS_PCR, the default, or FGS_THOMAS: sdr.h)
+    # engine extension: the FGS line solver (FGS_THOMAS, the default, or FGS_PCR: sdr.h)
     def getFgsSolver(self): return self._p.fgs_solver
     def setFgsSolver(self, v): self._set("fgs_solver", int(v))
 
@@ -145,16 +145,16 @@ def createDisparityWLSFilterGeneric(use_confidence: bool, device: int = 0) -> Di
     confidence-based variant (use_confidence=True) is implemented."""
     if not use_confidence:
         raise SDRError(-1, "createDisparityWLSFilterGeneric(false) is not implemented")
-    p = WlsParams(8000.0, 1.5, 24, 5, 0.001, 0.25, 3, 0, 0, 0, 0, 0, FGS_PCR)
+    p = WlsParams(8000.0, 1.5, 24, 5, 0.001, 0.25, 3, 0, 0, 0, 0, 0, FGS_THOMAS)
     return DisparityWLSFilter(p, device)
 
 
 def fastGlobalSmootherFilter(guide, src, lambda_, sigma_color, lambda_attenuation=0.25,
-                             num_iter=3, solver=FGS_PCR):
+                             num_iter=3, solver=FGS_THOMAS):
     """cv::ximgproc::fastGlobalSmootherFilter on a float32 (H, W) image (or (N, H, W) stack
     sharing one guide) with an 8-bit gray guide.  torch CUDA tensors are filtered on the current
-    stream; numpy arrays go through the current CUDA device.  solver: FGS_PCR (default) or
-    FGS_THOMAS (ximgproc's sequential elimination, bit for bit; include/sdr/sdr.h)."""
+    stream; numpy arrays go through the current CUDA device.  solver: FGS_THOMAS (default:
+    ximgproc's sequential elimination, bit for bit) or FGS_PCR (include/sdr/sdr.h)."""
     if torch is None:
         raise SDRError(-6, "fastGlobalSmootherFilter needs torch for device memory")
     host = not _is_cuda(src)

@@ -4,11 +4,14 @@
 The kernels evaluate every float operation in the oracle's order with contraction off, IEEE
 division and the oracle's host-computed weight table, so the filtered int16 map, the confidence
 map and raw FGS output are compared BIT FOR BIT -- for both line solvers: SDR_FGS_THOMAS
-(ximgproc's sequential elimination) against the oracle's fgs_line, SDR_FGS_PCR (the default,
-parallel cyclic reduction) against its fgs_line_pcr.  The two solvers themselves are compared at
-the north-star tolerance (<= 1 int16 level of the WLS output) in
-test_pcr_within_one_level_of_thomas.  Parity of the oracle itself against opencv_contrib is unpinned (no OpenCV in this image, no fixtures in the reference): see
-oracle/wls_oracle.h and tests/test_oracle_wls.py for how the restatement is pinned.
+(ximgproc's sequential elimination, the default since round 5) against the oracle's fgs_line,
+SDR_FGS_PCR (parallel cyclic reduction, opt-in) against its fgs_line_pcr.  The two solvers agree
+within 1 int16 level on the reference's own frames (test_pcr_within_one_level_of_thomas) but not
+where the confidence map is sparse (test_default_solver_hypothesis records how far PCR strays:
+hundreds of levels on some pixels, profiles/r5_pcr_vs_thomas.json), which is why the default is
+ximgproc's order.  Parity of the oracle itself against opencv_contrib is unpinned (no OpenCV in
+this image, no fixtures in the reference): see oracle/wls_oracle.h and tests/test_oracle_wls.py
+for how the restatement is pinned.
 """
 import numpy as np
 import pytest
@@ -125,8 +128,8 @@ def test_wls_filter_bit_exact_on_sgbm_maps(oracle, h, w, numD, seed, solver):
 
 @pytest.mark.parametrize("seed", list(range(1, 21)))
 def test_pcr_within_one_level_of_thomas(oracle, seed):
-    """The default solver against ximgproc's sequential one on the reference's own workload
-    (C0: 640x360 d=80 3WAY left + right matcher maps of a live-loop frame): the north-star
+    """The opt-in PCR solver against ximgproc's sequential one (the default) on the reference's own
+    workload (C0: 640x360 d=80 3WAY left + right matcher maps of a live-loop frame): the north-star
     tolerance, <= 1 int16 level (1/16 px) everywhere.  Both come from the device."""
     from stereo_depth_ruler_amd.synthetic import sbs_bgr_color_frame
     frame = sbs_bgr_color_frame(720, 1280, 80, seed=seed)
@@ -242,7 +245,8 @@ def test_create_wls_mutates_matcher():
 
 def test_wls_wide_roi_fallback(oracle):
     """A ROI wider than k_wls_prep / k_fgs_pcr take (4096 columns): the per-pixel front end and the
-    sequential solver, still bit-exact; the default PCR solver refuses it with SDR_ERR_SIZE."""
+    sequential solver (the default), still bit-exact; the opt-in PCR solver refuses it with
+    SDR_ERR_SIZE."""
     rng = np.random.default_rng(4)
     h, w = 6, 4200
     base = rng.integers(2, 40, (h, w // 8 + 1)) * 16
@@ -250,12 +254,78 @@ def test_wls_wide_roi_fallback(oracle):
     dr = -np.roll(dl, -2, 1)
     g = rng.integers(0, 256, (h, w)).astype(np.uint8)
     q = oracle.wls_params_for_sgbm(0, 32, 5, w, h, 8000.0, 1.1)
+    assert q.fgs_solver == FGS_THOMAS
     f = make_filter(q, w, h)
-    with pytest.raises(sdr.SDRError):
-        f.filter(dl, g, dr)
-    q.fgs_solver = FGS_THOMAS
-    f.setFgsSolver(FGS_THOMAS)
     ref, ref_conf = oracle.wls_filter(dl, dr, g, q, return_conf=True)
     got = f.filter(dl, g, dr)
     assert np.array_equal(bits(f.getConfidenceMap()), bits(ref_conf))
     assert np.array_equal(got, ref)
+    f.setFgsSolver(FGS_PCR)
+    with pytest.raises(sdr.SDRError):
+        f.filter(dl, g, dr)
+
+
+def _hyp_case(oracle, rng, W, H, guide, lam, sigma):
+    """A WLS input of the verdict's hypothesis space: flat, binary-edge, noise
+    or scene guides; block-constant disparities with 10 % invalid pixels (a sparse confidence map)
+    for the synthetic guides, the matcher pair of a synthetic frame for `scene`."""
+    D = 80
+    if guide == "scene":
+        L, dl, dr = sgbm_pair_maps(oracle, H, W, D, int(rng.integers(1 << 30)))
+        g = L
+    else:
+        if guide == "flat":
+            g = np.full((H, W), int(rng.integers(0, 256)), np.uint8)
+        elif guide == "edge":
+            g = np.zeros((H, W), np.uint8)
+            g[:, int(rng.integers(1, W)):] = 255
+            g[int(rng.integers(1, H)):, :] ^= 255
+        else:
+            g = rng.integers(0, 256, (H, W), dtype=np.uint8)
+        blocks = rng.integers(0, D * 16, ((H + 7) // 8, (W + 7) // 8))
+        dl = np.repeat(np.repeat(blocks, 8, 0), 8, 1)[:H, :W].astype(np.int16)
+        dl[rng.random((H, W)) < 0.1] = -16
+        dr = -np.clip(dl, 0, None).astype(np.int16)
+    q = oracle.wls_params_for_sgbm(0, D, 5, W, H, lam, sigma)
+    return g, dl, dr, q
+
+
+def test_default_solver_hypothesis(oracle):
+    """The default filter (createDisparityWLSFilter's parameters, SDR_FGS_THOMAS) bit-exact with the
+    oracle's sequential restatement over random shapes up to 4096-sample rows and columns, lambda in
+    [10, 2e4], sigma in [0.5, 5], flat / binary-edge / noise / scene guides; and the opt-in PCR
+    solver's distance from it on the same inputs, recorded (it exceeds 1 level on some cases:
+    that is why the default is ximgproc's order)."""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    worst = []
+
+    @settings(max_examples=24, deadline=None, derandomize=True,
+              suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+    @given(shape=st.sampled_from([(40, 61), (97, 130), (8, 3840), (6, 4096), (3840, 3), (4096, 2), (160, 560),
+                                  (33, 700)]),
+           guide=st.sampled_from(["flat", "edge", "noise", "scene"]),
+           loglam=st.floats(np.log(10.0), np.log(2e4)), sigma=st.floats(0.5, 5.0),
+           seed=st.integers(0, 1 << 20))
+    def run(shape, guide, loglam, sigma, seed):
+        H, W = shape
+        if guide == "scene" and (W < 100 or H < 8):
+            guide = "noise"  # the matcher needs columns past numDisparities
+        rng = np.random.default_rng(seed)
+        g, dl, dr, q = _hyp_case(oracle, rng, W, H, guide, float(np.exp(loglam)), sigma)
+        assert q.fgs_solver == FGS_THOMAS  # the oracle's default is ximgproc's order
+        ref = oracle.wls_filter(dl, dr, g, q)
+        f = make_filter(q, W, H)
+        assert f.getFgsSolver() == FGS_THOMAS
+        got = f.filter(dl, g, dr)
+        assert np.array_equal(got, ref), (shape, guide, (got != ref).sum())
+        if max(W, H) <= 4096 and q.roi_w > 0 and q.roi_h > 0:
+            f.setFgsSolver(FGS_PCR)
+            pcr = f.filter(dl, g, dr).astype(np.int32)
+            d = np.abs(pcr - ref.astype(np.int32))
+            worst.append((int(d.max()), float((d > 1).mean()), shape, guide))
+
+    run()
+    worst.sort(reverse=True)
+    print("PCR vs the sequential order, worst cases (levels, fraction > 1 level, shape, guide):", worst[:5])

@@ -237,6 +237,12 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_rig
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
                           double lambda, double sigma_color, double lambda_attenuation,
                           int num_iter, float* d_img, int nimg, int solver, void* stream);
+/* Self-test of the reciprocal the SDR_FGS_THOMAS coefficient jobs use (v_rcp_f32 + one Newton
+ * step, sdr_wls.hip fgs_rcp) against the IEEE quotient 1.0f / d, on the current device, for all
+ * 2^23 mantissas of d in [2^e, 2^(e+1)), 0 <= e <= 126: *mismatches = how many differ (0 expected
+ * for e <= 125, where 1/d is normal: the jobs' bit-exactness rests on it; SDR_FGS_THOMAS refuses
+ * lambda > 2^100 so that its pivots stay below 2^126). Synchronous. */
+int sdr_fgs_rcp_selftest(int e, unsigned int* mismatches);
 
 /* ---- ingest in front of the path: StereoRectifier + SBS split ----
  * cv::initUndistortRectifyMap(K, dist, R, P, size, CV_16SC2, map1, map2)   stereo_rectifier.cpp:7-11

@@ -1,6 +1,6 @@
 """FGS (fastGlobalSmootherFilter) device timing on the class path's shape: two right-hand sides of
 one 560x360 ROI (the C0/C4 WLS filter), both solvers.
-python scripts/fgs_bench.py [iters] [--lib PATH] [--thomas-only]"""
+python scripts/fgs_bench.py [iters] [--lib PATH] [--thomas-only] [--noise-guide]"""
 import sys
 import time
 
@@ -18,12 +18,20 @@ if "--lib" in args:
     _lib.use_library(args[i + 1])
     del args[i:i + 2]
 only = "--thomas-only" in args
-args = [a for a in args if a != "--thomas-only"]
+noise = "--noise-guide" in args
+args = [a for a in args if a not in ("--thomas-only", "--noise-guide")]
 it = int(args[0]) if args else 50
 rng = np.random.default_rng(0)
 h, w = 360, 560
 dev = torch.device("cuda", 0)
-g = torch.from_numpy(rng.integers(0, 256, (h, w)).astype(np.uint8)).to(dev)
+# the guide: the synthetic scene's left view (the matcher's input; --noise-guide: uniform noise,
+# every neighbour pair a random step, the sequential solver's slowest case)
+if noise:
+    g = torch.from_numpy(rng.integers(0, 256, (h, w)).astype(np.uint8)).to(dev)
+else:
+    from stereo_depth_ruler_amd import synthetic as S  # noqa: E402
+
+    g = torch.from_numpy(np.ascontiguousarray(S.make_pair(h, w, 64, seed=3)[0])).to(dev)
 x = torch.from_numpy((rng.random((2, h, w)) * 1000).astype(np.float32)).to(dev)
 for solver, name in ((FGS_PCR, "pcr"), (FGS_THOMAS, "thomas"))[1 if only else 0:]:
     for _ in range(3):

@@ -23,7 +23,7 @@ for _ in range(4):
     fastGlobalSmootherFilter(g, x, 8000.0, 1.1, solver=FGS_THOMAS)
 torch.cuda.synchronize()
 lib = ctypes.CDLL(sys.argv[1])
-buf = np.zeros((5, 1024), np.uint64)
+buf = np.zeros((6, 1024), np.uint64)
 assert lib.sdr_th_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0
 t0 = int(buf[0, 0])
 S = lambda r, i: (int(buf[r, i]) - t0) if buf[r, i] else None  # noqa: E731
@@ -33,4 +33,5 @@ for base, name in ((0, "forward"), (512, "back")):
     for c in range(64):
         if not buf[0, base + c]:
             break
-        print(c, S(0, base + c), S(1, base + c), S(2, base + c), S(3, base + c), S(4, base + c) if base == 0 else "")
+        print(c, S(0, base + c), S(1, base + c), S(2, base + c), S(3, base + c), S(4, base + c) if base == 0 else "",
+              "steps 0/16/32/48:" if base == 0 else "", [S(5, 8 * c + q) for q in range(4)] if base == 0 else "")

@@ -131,6 +131,7 @@ SIGNATURES = [
     ("sdr_write_pcd_binary", _i, [_c.c_char_p, _vp, _i, _i]),
     ("sdr_fgs_filter_device", _i, [_vp, _sz, _i, _i, _c.c_double, _c.c_double, _c.c_double, _i,
                                    _vp, _i, _i, _vp]),
+    ("sdr_fgs_rcp_selftest", _i, [_i, _c.POINTER(_c.c_uint)]),
     ("sdr_colormap_lut", _i, [_i, _vp]),
     ("sdr_display_create", _i, [_i, _c.POINTER(_vp)]),
     ("sdr_display_destroy", _i, [_vp]),

@@ -222,7 +222,18 @@ static_assert(kThLds <= 160 * 1024, "one workgroup's LDS");
 constexpr int kFgsMaxJobs = 8;         // coefficient jobs in one launch
 constexpr size_t kFgsOverread = 4096;  // bytes past a k-major array the loaders may read (the
                                        // last workgroup's lines beyond st, at the last sample)
+constexpr double kFgsThomasMaxLambda = 0x1p100;  // pivots below 2^126 (fgs_rcp)
 constexpr uint32_t kFgsTinyKey = 0x1EFFFFFFu;  // fgs_tiny_key(q) < this <=> 0 < |q| < 2^-96
+
+// The correctly rounded 1/d for 1 <= d < 2^126: v_rcp_f32 and one Newton step, equal to the IEEE
+// quotient 1.0f / d for every mantissa of d at every exponent checked (sdr_fgs_rcp_selftest,
+// tests/test_gpu_wls.py; at 2^126 and beyond 1/d is subnormal and it is not) -- 3 operations
+// instead of the IEEE division's ~11.  Every pivot is at most 1 + 2 * lambda, hence
+// kFgsThomasMaxLambda.
+__device__ __forceinline__ float fgs_rcp(float d) {
+    const float r0 = __builtin_amdgcn_rcpf(d);
+    return __builtin_fmaf(__builtin_fmaf(-d, r0, 1.0f), r0, r0);
+}
 
 // 2|q| - 1 as an integer (the sign bit shifted out): below kFgsTinyKey exactly when 0 < |q| < 2^-96
 // (+-0 wraps to the largest key); the minimum over a chunk decides the redo
@@ -297,6 +308,7 @@ __device__ unsigned long long* g_th_stamps;
         if (g_th_stamps && blockIdx.x == 0 && blockIdx.y == 0 && (threadIdx.x & 63) == 0)         \
             g_th_stamps[(role) * 1024 + (idx)] = __builtin_amdgcn_s_memtime();                    \
     } while (0)
+constexpr int kThStampRoles = 6;
 #else
 #define TH_STAMP(role, idx) \
     do {                    \
@@ -332,10 +344,12 @@ template <int IW> __device__ __forceinline__ void th_wait_chunks(int m) {
 
 // A loader wave over one phase of nch chunks (chunk c = samples k0 + dk * (c * CH + j)): chunks
 // 0 .. kThNB-2 ahead, then per iteration c chunk c + kThNB - 1 into the buffer chunk c - 1 left,
-// and chunk c + 2 landed before the barrier; 1 + nch barriers, as every wave of the phase.
+// and chunk c + 2 landed before the barrier; 1 + extra + nch barriers, as every wave of the phase.
+// (not inlined: with the loaders' DMA in the kernel body the compiler's wait analysis, merging
+// paths, put a vmcnt(0) before LDS writes of the other waves' code -- every row of a job)
 template <int LPB, int ES0, int ES1>
-__device__ __forceinline__ void th_load_phase(const char* g0, const char* g1, size_t st, int l0, int k0, int dk,
-                                              int last, int nch, char* lds, int lw, int lane) {
+__device__ __noinline__ void th_load_phase(const char* g0, const char* g1, size_t st, int l0, int k0, int dk,
+                                              int last, int nch, char* lds, int lw, int lane, int extra = 0) {
     constexpr int CH = 1024 / LPB, IW = (ES0 + ES1) / 2;
     auto issue = [&](int c) __attribute__((always_inline)) {
         char* buf = lds + (c % kThNB) * kThBuf;
@@ -346,6 +360,7 @@ __device__ __forceinline__ void th_load_phase(const char* g0, const char* g1, si
     for (int c = 0; c < pre; c++) issue(c);
     th_wait_chunks<IW>(pre - 2);
     th_barrier();
+    for (int i = 0; i < extra; i++) th_barrier();  // (a job's flag barrier)
     for (int c = 0; c < nch; c++) {
         if (c + kThNB - 1 < nch) issue(c + kThNB - 1);
         if (lw == 0) TH_STAMP(2, (dk < 0 ? 512 : 0) + c);
@@ -436,15 +451,27 @@ __device__ __forceinline__ void th_write_back_phase(const FgsThArgs& a, size_t f
     if (nch > 0) put(nch - 1);
 }
 
+// A coefficient job.  Its pivots' reciprocal is fgs_rcp and t = cc / den comes from it
+// (Markstein) -- exact unless cc / den can fall below ~2^-96, which happens only when cc = lam * C
+// is tiny (the weights of gray-level steps of ~80 and more at sigma 1.1).  The writer flags each
+// chunk holding such a weight on any of the workgroup's lines (kThJobFlags in LDS, one word per
+// chunk parity; chunk c + 1's during iteration c, chunk 0's between two prologue barriers) and the
+// solver runs a flagged chunk with IEEE divisions, a clean one with no per-sample test or branch
+// (a branch a sample cost more than the divisions it saved: 63 us a 560-sample job launch on a
+// noise guide, 48 on a scene).
+constexpr int kThJobFlags = kThRows - 16;  // byte offset of the two flag words in the rows area
+static_assert(2 * 1024 * 16 <= kThJobFlags, "the job rows and their flags");
+
 template <int LPB>
-__device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t fofs, int l0, int nch, const char* orow,
-                                                   int lane) {
+__device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t fofs, int l0, int nch, const char* lds,
+                                                   char* orow, int lane) {
     constexpr int CH = 1024 / LPB;
     const int line = lane % LPB, last = J.n - 1;
     const bool lv = l0 + line < J.nl;
     float4* co = J.coef + fofs + l0 + line;
     float* tt = J.tt + fofs + l0 + line;
     const size_t st = (size_t)J.st;
+    const float lam = J.lam, tiny = 0x1p-96f * (1.0f + 2.0f * lam);
     auto put = [&](int c) __attribute__((always_inline)) {
         const char* rows = orow + (c & 1) * 1024 * 16;
 #pragma unroll 4
@@ -458,9 +485,31 @@ __device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t f
             }
         }
     };
+    // chunk c's weights (1024 floats, 16 a lane): any tiny lam * C on a real line and sample
+    auto flag = [&](int c) __attribute__((always_inline)) {
+        const float* cw = (const float*)(lds + (c % kThNB) * kThBuf);
+        bool t = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int e0 = (q * 64 + lane) * 4;  // element j * LPB + l
+            const float4 v = *(const float4*)(cw + e0);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float x = lam * (&v.x)[e];
+                const int el = e0 + e, j = el / LPB, l = el % LPB;
+                t = t || (fabsf(x) < tiny && x != 0.0f && c * CH + j <= last && l0 + l < J.nl);
+            }
+        }
+        if (lane == 0) *(int*)(orow + kThJobFlags + (c & 1) * 4) = __builtin_amdgcn_ballot_w64(t) != 0;
+    };
+    th_barrier();
+    if (nch > 0) flag(0);
+    th_lgkm0();
     th_barrier();
     for (int c = 0; c < nch; c++) {
         if (c > 0) put(c - 1);
+        if (c + 1 < nch) flag(c + 1);
+        th_lgkm0();
         th_barrier();
     }
     if (nch > 0) put(nch - 1);
@@ -476,6 +525,7 @@ __device__ __forceinline__ void th_job_solver(const FgsCoefJob& J, int l0, int l
     const float lam = J.lam;
     float rc[kThPF];
     th_barrier();
+    th_barrier();  // (chunk 0's flag)
 #pragma unroll
     for (int j = 0; j < kThPF; j++) rc[j] = *(const float*)(lds + (j * LPB + ln) * 4);
     float cprev = 0.0f, tprev = 0.0f;
@@ -484,9 +534,12 @@ __device__ __forceinline__ void th_job_solver(const FgsCoefJob& J, int l0, int l
         const char* nxt = lds + ((c + 1) % kThNB) * kThBuf;
         const int kc = c * CH;
         char* w = orow + (c & 1) * 1024 * 16 + ln * 16;
-        auto body = [&](auto guard) __attribute__((always_inline)) {
+        TH_STAMP(0, c);
+        // a chunk with a tiny weight divides (IEEE), a clean one takes the reciprocal form
+        auto body = [&](auto guard, auto exact) __attribute__((always_inline)) {
 #pragma unroll
             for (int j = 0; j < CH; j++) {
+                if (j % 16 == 0) TH_STAMP(5, c * 8 + j / 16);
                 const float cw = rc[j % kThPF];
                 const int jn = j + kThPF;
                 rc[j % kThPF] = jn < CH ? *(const float*)(cur + (jn * LPB + ln) * 4)
@@ -495,14 +548,27 @@ __device__ __forceinline__ void th_job_solver(const FgsCoefJob& J, int l0, int l
                     const float aa = lam * cprev;
                     const float cc = lam * cw;
                     const float den = (1.0f - cc) - aa * (1.0f + tprev);
-                    tprev = cc / den;
-                    *(float4*)(w + j * LPB * 16) = make_float4(aa, den, 1.0f / den, tprev);
+                    const float r = fgs_rcp(den);
+                    if constexpr (decltype(exact)::value) {
+                        tprev = cc / den;
+                    } else {
+                        const float q0 = cc * r;
+                        tprev = __builtin_fmaf(-__builtin_fmaf(q0, den, -cc), r, q0);  // cc / den
+                    }
+                    *(float4*)(w + j * LPB * 16) = make_float4(aa, den, r, tprev);
                     cprev = cw;
                 }
             }
         };
-        if (kc + CH - 1 <= last) body(std::false_type{});
-        else body(std::true_type{});
+        const bool full = kc + CH - 1 <= last;
+        if (*(const volatile int*)(orow + kThJobFlags + (c & 1) * 4)) {
+            if (full) body(std::false_type{}, std::true_type{});
+            else body(std::true_type{}, std::true_type{});
+        } else {
+            if (full) body(std::false_type{}, std::false_type{});
+            else body(std::true_type{}, std::false_type{});
+        }
+        TH_STAMP(1, c);
         th_lgkm0();
         th_barrier();
     }
@@ -553,6 +619,7 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
         auto body = [&](auto guard) __attribute__((always_inline)) {
 #pragma unroll
             for (int j = 0; j < CH; j++) {
+                if (j % 16 == 0) TH_STAMP(5, c * 8 + j / 16);
                 const int r = j % kThPF;
                 const V xu = ru[r];
                 const float4 xq = rq[r];  // a, den, 1/den, t
@@ -560,28 +627,16 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
                 if (jn < CH) rd(cur, jn, r);
                 else rd(nxt, jn - CH, r);
                 if (!decltype(guard)::value || kc + j <= last) {
-#ifdef SDR_TH_EXP_NOCHAIN
-                    p0 = R::x(xu) + xq.x;
-                    p1 = R::y(xu) + xq.y;
-                    if (false) {
-#else
-                    {
-#endif
                     const float x0 = R::x(xu) - xq.x * p0;
                     const float q00 = x0 * xq.z;
                     p0 = __builtin_fmaf(-__builtin_fmaf(q00, xq.y, -x0), xq.z, q00);
-                    uint32_t kk = fgs_tiny_key(q00);
+                    key = min(key, fgs_tiny_key(q00));
                     if constexpr (TWO) {
                         const float x1 = R::y(xu) - xq.x * p1;
                         const float q01 = x1 * xq.z;
                         p1 = __builtin_fmaf(-__builtin_fmaf(q01, xq.y, -x1), xq.z, q01);
-                        kk = min(kk, fgs_tiny_key(q01));
+                        key = min(key, fgs_tiny_key(q01));
                     }
-                    key = min(key, kk);
-                    }
-#ifdef SDR_TH_EXP_MASKW
-                    if (lane < LPB)
-#endif
                     *(V*)(wu + j * LPB * ESU) = R::make(p0, p1);
                 }
             }
@@ -645,9 +700,6 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
                 if (!decltype(guard)::value || kb - j >= 0) {
                     q0 = R::x(xu) - xt * q0;
                     if constexpr (TWO) q1 = R::y(xu) - xt * q1;
-#ifdef SDR_TH_EXP_MASKW
-                    if (lane < LPB)
-#endif
                     *(V*)(rows + j * RW::S * 4) = R::make(q0, q1);
                 }
             }
@@ -681,8 +733,8 @@ __global__ __launch_bounds__(256) void k_fgs_th(FgsThArgs a) {
         if (wave == 0) th_job_solver<LPB>(J, l0, lane, lds, orow);
         else if (wave <= 2)
             th_load_phase<LPB, 4, 0>((const char*)(J.Cw + fofs), nullptr, J.st, l0, 0, 1, J.n - 1, nch, lds,
-                                     wave - 1, lane);
-        else th_write_job_phase<LPB>(J, fofs, l0, nch, orow, lane);
+                                     wave - 1, lane, 1);
+        else th_write_job_phase<LPB>(J, fofs, l0, nch, lds, orow, lane);
         return;
     }
     constexpr int ESU = TWO ? 8 : 4;
@@ -1165,7 +1217,7 @@ static void launch_fgs_th(FgsThArgs a, bool pass, bool two, int F, hipStream_t s
         static int launches = 0;
         static unsigned long long* buf = nullptr;
         static const int want = getenv("SDR_TH_STAMP_LAUNCH") ? atoi(getenv("SDR_TH_STAMP_LAUNCH")) : -1;
-        if (!buf) (void)hipMalloc((void**)&buf, 5 * 1024 * 8);
+        if (!buf) (void)hipMalloc((void**)&buf, kThStampRoles * 1024 * 8);
         unsigned long long* v = launches++ == want ? buf : nullptr;
         (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_th_stamps), &v, sizeof(v), 0, hipMemcpyHostToDevice, st);
         th_stamp_buf = buf;
@@ -1355,6 +1407,8 @@ namespace {
 int check_wls_params(const sdr_wls_params& p) {
     if (!(p.lambda >= 0.0) || !(p.sigma_color >= 0.0) || p.num_iter < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
+    if (p.fgs_solver == SDR_FGS_THOMAS && p.lambda > sdr::kFgsThomasMaxLambda)
+        return sdr::set_error(SDR_ERR_ARG, "SDR_FGS_THOMAS takes lambda <= 2^100 (its pivots stay below 2^126)");
     if (p.fgs_solver != SDR_FGS_PCR && p.fgs_solver != SDR_FGS_THOMAS)
         return sdr::set_error(SDR_ERR_ARG, "fgs_solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
     if (p.depth_discontinuity_radius < 0 || p.left_offset < 0 || p.right_offset < 0 ||
@@ -1620,11 +1674,37 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* dl, const int16_t* dr, const uint8
     return SDR_OK;
 }
 
+// sdr_fgs_rcp_selftest: fgs_rcp against the IEEE division for all 2^23 mantissas of d in
+// [2^e, 2^(e+1))
+namespace sdr {
+__global__ __launch_bounds__(256) void k_fgs_rcp_check(int e, unsigned int* bad) {
+    const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+    const float d = __builtin_bit_cast(float, (uint32_t)(127 + e) << 23 | m);
+    const volatile float one = 1.0f;
+    if (__builtin_bit_cast(uint32_t, fgs_rcp(d)) != __builtin_bit_cast(uint32_t, one / d)) atomicAdd(bad, 1u);
+}
+}  // namespace sdr
+
+int sdr_fgs_rcp_selftest(int e, unsigned int* mismatches) {
+    if (!mismatches || e < 0 || e > 126) return sdr::set_error(SDR_ERR_ARG, "e must be in [0, 126]");
+    unsigned int* d = nullptr;
+    WLS_HIP(hipMalloc((void**)&d, 4));
+    hipError_t err = hipMemset(d, 0, 4);
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(sdr::k_fgs_rcp_check, dim3((1u << 23) / 256), dim3(256), 0, 0, e, d);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipMemcpy(mismatches, d, 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    WLS_HIP(err);
+    return SDR_OK;
+}
+
 #ifdef SDR_TH_STAMPS
 // diagnostic build only: the stamps of the launch SDR_TH_STAMP_LAUNCH names ([5][1024] u64)
 int sdr_th_stamps(unsigned long long* host) {
     if (!sdr::th_stamp_buf) return -1;
-    return hipMemcpy(host, sdr::th_stamp_buf, 5 * 1024 * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+    return hipMemcpy(host, sdr::th_stamp_buf, sdr::kThStampRoles * 1024 * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -1636,6 +1716,8 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
         return sdr::set_error(SDR_ERR_ARG, "bad size/stride");
     if (!(lambda >= 0.0) || !(sigma >= 0.0) || iters < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
+    if (solver == SDR_FGS_THOMAS && lambda > sdr::kFgsThomasMaxLambda)
+        return sdr::set_error(SDR_ERR_ARG, "SDR_FGS_THOMAS takes lambda <= 2^100 (its pivots stay below 2^126)");
     if (solver != SDR_FGS_PCR && solver != SDR_FGS_THOMAS)
         return sdr::set_error(SDR_ERR_ARG, "solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
     if (solver == SDR_FGS_PCR && (w > sdr::kPcrMaxN || h > sdr::kPcrMaxN))

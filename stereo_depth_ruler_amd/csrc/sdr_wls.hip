@@ -218,6 +218,11 @@ constexpr int kThRows = ThRows<16, 8>::bytes;  // the rows area (the largest use
 constexpr int kThLds = kThNB * kThBuf + kThRows;
 static_assert(ThRows<32, 8>::bytes <= kThRows && ThRows<64, 8>::bytes <= kThRows, "rows");
 static_assert(kThRows >= 2 * 1024 * 16, "the forward and job rows fit the rows area");
+// two flag words (chunk parity) in the rows area's last bytes -- padding of the back substitution's
+// last row, clear of the job rows: a job chunk to run with IEEE divisions
+constexpr int kThFlags = kThRows - 16;
+
+static_assert(2 * 1024 * 16 <= kThFlags && ThRows<16, 8>::S * 4 - 16 >= 16 * 8, "flags in the rows' padding");
 static_assert(kThLds <= 160 * 1024, "one workgroup's LDS");
 constexpr int kFgsMaxJobs = 8;         // coefficient jobs in one launch
 constexpr size_t kFgsOverread = 4096;  // bytes past a k-major array the loaders may read (the
@@ -309,9 +314,17 @@ __device__ unsigned long long* g_th_stamps;
             g_th_stamps[(role) * 1024 + (idx)] = __builtin_amdgcn_s_memtime();                    \
     } while (0)
 constexpr int kThStampRoles = 6;
+__device__ unsigned int g_th_counts[4];  // pass chunks: reciprocal form, exact from the start, redone
+#define TH_COUNT(i)                                                                                \
+    do {                                                                                           \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_th_counts[i], 1u);                               \
+    } while (0)
 #else
 #define TH_STAMP(role, idx) \
     do {                    \
+    } while (0)
+#define TH_COUNT(i) \
+    do {            \
     } while (0)
 #endif
 
@@ -454,13 +467,11 @@ __device__ __forceinline__ void th_write_back_phase(const FgsThArgs& a, size_t f
 // A coefficient job.  Its pivots' reciprocal is fgs_rcp and t = cc / den comes from it
 // (Markstein) -- exact unless cc / den can fall below ~2^-96, which happens only when cc = lam * C
 // is tiny (the weights of gray-level steps of ~80 and more at sigma 1.1).  The writer flags each
-// chunk holding such a weight on any of the workgroup's lines (kThJobFlags in LDS, one word per
+// chunk holding such a weight on any of the workgroup's lines (kThFlags in LDS, one word per
 // chunk parity; chunk c + 1's during iteration c, chunk 0's between two prologue barriers) and the
 // solver runs a flagged chunk with IEEE divisions, a clean one with no per-sample test or branch
 // (a branch a sample cost more than the divisions it saved: 63 us a 560-sample job launch on a
 // noise guide, 48 on a scene).
-constexpr int kThJobFlags = kThRows - 16;  // byte offset of the two flag words in the rows area
-static_assert(2 * 1024 * 16 <= kThJobFlags, "the job rows and their flags");
 
 template <int LPB>
 __device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t fofs, int l0, int nch, const char* lds,
@@ -500,7 +511,7 @@ __device__ __forceinline__ void th_write_job_phase(const FgsCoefJob& J, size_t f
                 t = t || (fabsf(x) < tiny && x != 0.0f && c * CH + j <= last && l0 + l < J.nl);
             }
         }
-        if (lane == 0) *(int*)(orow + kThJobFlags + (c & 1) * 4) = __builtin_amdgcn_ballot_w64(t) != 0;
+        if (lane == 0) *(int*)(orow + kThFlags + (c & 1) * 4) = __builtin_amdgcn_ballot_w64(t) != 0;
     };
     th_barrier();
     if (nch > 0) flag(0);
@@ -561,7 +572,7 @@ __device__ __forceinline__ void th_job_solver(const FgsCoefJob& J, int l0, int l
             }
         };
         const bool full = kc + CH - 1 <= last;
-        if (*(const volatile int*)(orow + kThJobFlags + (c & 1) * 4)) {
+        if (*(const volatile int*)(orow + kThFlags + (c & 1) * 4)) {
             if (full) body(std::false_type{}, std::true_type{});
             else body(std::true_type{}, std::true_type{});
         } else {
@@ -616,7 +627,10 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
         TH_STAMP(0, c);
         const float ps0 = p0, ps1 = p1;
         uint32_t key = 0xffffffffu;
-        auto body = [&](auto guard) __attribute__((always_inline)) {
+        // exact: IEEE divisions (the right-hand sides decayed into the range the reciprocal form
+        // does not cover: long runs of zero confidence); otherwise the reciprocal form with the
+        // tiny-quotient key
+        auto body = [&](auto guard, auto exact) __attribute__((always_inline)) {
 #pragma unroll
             for (int j = 0; j < CH; j++) {
                 if (j % 16 == 0) TH_STAMP(5, c * 8 + j / 16);
@@ -628,33 +642,47 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
                 else rd(nxt, jn - CH, r);
                 if (!decltype(guard)::value || kc + j <= last) {
                     const float x0 = R::x(xu) - xq.x * p0;
-                    const float q00 = x0 * xq.z;
-                    p0 = __builtin_fmaf(-__builtin_fmaf(q00, xq.y, -x0), xq.z, q00);
-                    key = min(key, fgs_tiny_key(q00));
-                    if constexpr (TWO) {
-                        const float x1 = R::y(xu) - xq.x * p1;
-                        const float q01 = x1 * xq.z;
-                        p1 = __builtin_fmaf(-__builtin_fmaf(q01, xq.y, -x1), xq.z, q01);
-                        key = min(key, fgs_tiny_key(q01));
+                    const float x1 = TWO ? R::y(xu) - xq.x * p1 : 0.0f;
+                    if constexpr (decltype(exact)::value) {
+                        p0 = x0 / xq.y;
+                        if constexpr (TWO) p1 = x1 / xq.y;
+                    } else {
+                        const float q00 = x0 * xq.z;
+                        p0 = __builtin_fmaf(-__builtin_fmaf(q00, xq.y, -x0), xq.z, q00);
+                        key = min(key, fgs_tiny_key(q00));
+                        if constexpr (TWO) {
+                            const float q01 = x1 * xq.z;
+                            p1 = __builtin_fmaf(-__builtin_fmaf(q01, xq.y, -x1), xq.z, q01);
+                            key = min(key, fgs_tiny_key(q01));
+                        }
                     }
                     *(V*)(wu + j * LPB * ESU) = R::make(p0, p1);
                 }
             }
         };
-        if (kc + CH - 1 <= last) body(std::false_type{});
-        else body(std::true_type{});
-        // a chunk with a quotient the reciprocal form does not cover (rare: right-hand sides
-        // decayed below 2^-96) runs again from its start with real divisions, its rows
-        // overwriting the first run's (the chunk's buffer is intact until the barrier)
-        if (__builtin_amdgcn_ballot_w64(valid && key < kFgsTinyKey)) {
-            p0 = ps0;
-            p1 = ps1;
-            for (int j = 0; j < CH && kc + j <= last; j++) {
-                const V xu = rdu(cur, j);
-                const float4 xq = rdq(cur, j);
-                p0 = (R::x(xu) - xq.x * p0) / xq.y;
-                if constexpr (TWO) p1 = (R::y(xu) - xq.x * p1) / xq.y;
-                *(V*)(wu + j * LPB * ESU) = R::make(p0, p1);
+        const bool full = kc + CH - 1 <= last;
+        // a chunk starting from values already small (|p| < 2^-64) is likely to decay through the
+        // uncovered range: it divides from the start
+        const uint32_t small = 0x3EFFFFFFu;  // fgs_tiny_key(q) < small <=> 0 < |q| < 2^-64
+        if (__builtin_amdgcn_ballot_w64(valid && (fgs_tiny_key(p0) < small || (TWO && fgs_tiny_key(p1) < small)))) {
+            TH_COUNT(1);
+            if (full) body(std::false_type{}, std::true_type{});
+            else body(std::true_type{}, std::true_type{});
+        } else {
+            if (full) body(std::false_type{}, std::false_type{});
+            else body(std::true_type{}, std::false_type{});
+            // a chunk with a quotient the reciprocal form does not cover runs again from its start
+            // with real divisions, its rows overwriting the first run's (the chunk's buffer is
+            // intact until the barrier; the operand ring restarts at its first slots)
+            TH_COUNT(0);
+            if (__builtin_amdgcn_ballot_w64(valid && key < kFgsTinyKey)) {
+                TH_COUNT(2);
+                p0 = ps0;
+                p1 = ps1;
+#pragma unroll
+                for (int j = 0; j < kThPF; j++) rd(cur, j, j);
+                if (full) body(std::false_type{}, std::true_type{});
+                else body(std::true_type{}, std::true_type{});
             }
         }
         TH_STAMP(1, c);
@@ -1702,6 +1730,9 @@ int sdr_fgs_rcp_selftest(int e, unsigned int* mismatches) {
 
 #ifdef SDR_TH_STAMPS
 // diagnostic build only: the stamps of the launch SDR_TH_STAMP_LAUNCH names ([5][1024] u64)
+int sdr_th_counts(unsigned int* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_counts), 16, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 int sdr_th_stamps(unsigned long long* host) {
     if (!sdr::th_stamp_buf) return -1;
     return hipMemcpy(host, sdr::th_stamp_buf, sdr::kThStampRoles * 1024 * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;

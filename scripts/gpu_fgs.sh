@@ -1,7 +1,8 @@
 #!/bin/bash
-# round 5: LDS-staged sequential FGS passes: parity, then per-kernel durations (scene and noise guides)
+# The sequential FGS (SDR_FGS_THOMAS): WLS parity, then per-launch durations on a scene and a noise guide
+# (python scripts/th_trace.py gpurun_out/fgs/prof/fgs_kernel_trace.csv)
 set -o pipefail
-O=gpurun_out/r5g
+O=gpurun_out/fgs
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 100 --timeout-method thread tests/test_gpu_wls.py \

@@ -3,7 +3,7 @@
 # passes (FETCH_SIZE / WRITE_SIZE, one counter group a run, no tracing) of C2 and C3.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r5finB
+O=gpurun_out/round_end_b
 mkdir -p $O
 prof() {  # name, bench args
   local n=$1; shift

@@ -38,3 +38,13 @@ if lib.sdr_th_stamps(buf.ctypes.data_as(ctypes.c_void_p)) == 0 and buf[0, 0]:
                 break
             print(c, S_(0, base + c), S_(1, base + c), S_(2, base + c), S_(3, base + c),
                   S_(4, base + c) if base == 0 else "", [S_(5, 8 * c + q) for q in range(4)] if base == 0 else "")
+blk = np.zeros((512, 3), np.uint64)
+if lib.sdr_th_blocks(blk.ctypes.data_as(ctypes.c_void_p)) == 0 and blk[0, 0]:
+    used = [i for i in range(512) if blk[i, 0]]
+    t0 = min(int(blk[i, 0]) for i in used)
+    rows = sorted(((int(blk[i, 2]) - int(blk[i, 0]), int(blk[i, 1]) - int(blk[i, 0]), int(blk[i, 0]) - t0, i) for i in used),
+                  reverse=True)
+    print("workgroups of the stamped launch, slowest first: (total cycles, forward cycles, start offset, block)")
+    for r in rows[:8]:
+        print("  ", r)
+    print("   fastest:", rows[-3:])

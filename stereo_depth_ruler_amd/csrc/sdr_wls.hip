@@ -314,6 +314,12 @@ __device__ unsigned long long* g_th_stamps;
             g_th_stamps[(role) * 1024 + (idx)] = __builtin_amdgcn_s_memtime();                    \
     } while (0)
 constexpr int kThStampRoles = 6;
+__device__ unsigned long long g_th_blk[512][3];  // per workgroup of the stamped launch: start, fwd end, end
+#define TH_BLK(i)                                                                                  \
+    do {                                                                                           \
+        if (g_th_stamps && blockIdx.y == 0 && (threadIdx.x & 63) == 0 && blockIdx.x < 512)         \
+            g_th_blk[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                                \
+    } while (0)
 __device__ unsigned int g_th_counts[4];  // pass chunks: reciprocal form, exact from the start, redone
 #define TH_COUNT(i)                                                                                \
     do {                                                                                           \
@@ -325,6 +331,9 @@ __device__ unsigned int g_th_counts[4];  // pass chunks: reciprocal form, exact 
     } while (0)
 #define TH_COUNT(i) \
     do {            \
+    } while (0)
+#define TH_BLK(i) \
+    do {          \
     } while (0)
 #endif
 
@@ -609,6 +618,7 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
         return *(const float4*)(buf + S1 + (j * LPB + ln) * 16);
     };
     // ---- forward elimination ----
+    TH_BLK(0);
     V ru[kThPF];
     float4 rq[kThPF];
     auto rd = [&](const char* buf, int j, int r) __attribute__((always_inline)) {
@@ -690,6 +700,7 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
         th_barrier();
     }
     // (the writer has the forward values in memory before this barrier)
+    TH_BLK(1);
     th_barrier();
     // ---- back substitution: u_k -= t[k] * u_{k+1}, k = n-2 .. 0 (the last sample keeps p) ----
     if (valid) {
@@ -738,6 +749,7 @@ __device__ __forceinline__ void th_pass_solver(const FgsThArgs& a, size_t fofs, 
         th_lgkm0();
         th_barrier();
     }
+    TH_BLK(2);
 }
 
 // One FGS pass (all lines of F frames) in ximgproc's order from its jobs' coefficients; blocks
@@ -1730,6 +1742,9 @@ int sdr_fgs_rcp_selftest(int e, unsigned int* mismatches) {
 
 #ifdef SDR_TH_STAMPS
 // diagnostic build only: the stamps of the launch SDR_TH_STAMP_LAUNCH names ([5][1024] u64)
+int sdr_th_blocks(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_blk), 512 * 3 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 int sdr_th_counts(unsigned int* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_counts), 16, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }

@@ -41,6 +41,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 #                 (stereo_displayer.cpp:155-162, the reference app's per-frame loop)
 #   kind "cloud": side-by-side BGR -> gray -> compute -> reproject(handleMissing) ->
 #                 convertCVMatToPCL(left) -> VoxelGrid(5 mm)   (pcd_write.cpp:81-130)
+# frames in flight a config defaults to (--streams), from round-5 sweeps on one MI355X
+# (profiles/r5_streams_sweep.md): C2 is flat from 2 to 6 (1737-1772 fps); the class path's frame
+# (C4: ~30 short launches, the sequential FGS passes a few hundred workgroups each) fills the chip
+# only with more frames beside it, 2367 fps at 3 and 3592-3651 at 6
+STREAMS_DEFAULT = {"c4": 6}
+
 CONFIGS = {
     "c2": ("C2 (BASELINE configs[1]): 1280x720 d=128 MODE_SGBM 5-path + reprojectImageTo3D(Q, "
            "handleMissing), batch 1", 1280, 720, (0, 128, 5, 600, 2400, 1, 63, 12, 200, 2, 0), 1, True, "sgbm"),
@@ -249,7 +255,8 @@ def parse_args(argv=None):
     ap.add_argument("--in-flight-timing", action="store_true",
                     help="also put HIP events around matcher 0's launches inside the timed region "
                          "(roofline.in_flight; the events cost ~2 %% of the frame rate)")
-    ap.add_argument("--streams", type=int, default=3, help="frames in flight (one matcher + stream each)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="frames in flight (one matcher + stream each); default per config (STREAMS_DEFAULT)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
     ap.add_argument("--stream-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="time a 2 GiB device copy after the run (roofline.stream_probe: this box's "
@@ -339,7 +346,7 @@ def main():
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
     D, mode = args[1], args[10]
     nf = max(a.frames, batch)
-    ns = max(1, a.streams)
+    ns = max(1, a.streams if a.streams is not None else STREAMS_DEFAULT.get(a.config, 3))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
     gather_bytes = batch * H * W * 2  # int16 disparity per step
     if kind == "sgbm":

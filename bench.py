@@ -453,6 +453,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(a.warmup + i)
+    host_el = time.perf_counter() - t0  # the host's enqueue time (the GPU may still be running)
     for p in pending:
         if p is not None:
             p.wait()
@@ -694,6 +695,8 @@ def main():
             "streams_per_gpu": ns,
         },
         "fps": round(world * a.steps * batch / el, 2),
+        # rank 0's enqueue loop alone: near ms_per_step means the host's launch rate bounds the line
+        "host_enqueue_ms_per_step": round(host_el / a.steps * 1e3, 4),
         "ranks": ranks,
         "gather_check": gather_check,
         "roofline": roofline,

@@ -62,3 +62,11 @@ def test_world_size_must_match_gpus():
 def test_gpus_must_be_positive():
     with pytest.raises(SystemExit):
         bench.parse_args(["--gpus", "0"])
+
+
+def test_frames_in_flight_default_per_config():
+    # --streams unset: the config's measured default (profiles/r5_streams_sweep.md), 3 otherwise
+    assert bench.parse_args([]).streams is None
+    assert bench.STREAMS_DEFAULT.get("c4") == 6
+    assert all(c in bench.CONFIGS for c in bench.STREAMS_DEFAULT)
+    assert bench.parse_args(["--config", "c4", "--streams", "2"]).streams == 2

@@ -257,6 +257,8 @@ def parse_args(argv=None):
                          "(roofline.in_flight; the events cost ~2 %% of the frame rate)")
     ap.add_argument("--streams", type=int, default=None,
                     help="frames in flight (one matcher + stream each); default per config (STREAMS_DEFAULT)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step instead of the config's (experiments; the workload string says so)")
     ap.add_argument("--iso-steps", type=int, default=30, help="single-stream steps for roofline.isolated")
     ap.add_argument("--stream-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="time a 2 GiB device copy after the run (roofline.stream_probe: this box's "
@@ -344,6 +346,12 @@ def main():
                     "fgs_pass": _sg.KERNEL_FGS, "k_wls_final": _sg.KERNEL_WLS_FINAL}
 
     desc, W, H, args, batch, hm, kind = CONFIGS[a.config]
+    if a.batch is not None:
+        # (an experiment knob: the BASELINE configs' lines use their own batch)
+        if a.batch < 1:
+            raise SystemExit("bench: --batch must be >= 1")
+        batch = a.batch
+        desc = f"{desc} [--batch {batch}: not the config's own batch]"
     D, mode = args[1], args[10]
     nf = max(a.frames, batch)
     ns = max(1, a.streams if a.streams is not None else STREAMS_DEFAULT.get(a.config, 3))

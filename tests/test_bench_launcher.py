@@ -70,3 +70,8 @@ def test_frames_in_flight_default_per_config():
     assert bench.STREAMS_DEFAULT.get("c4") == 6
     assert all(c in bench.CONFIGS for c in bench.STREAMS_DEFAULT)
     assert bench.parse_args(["--config", "c4", "--streams", "2"]).streams == 2
+
+
+def test_batch_override_is_opt_in():
+    assert bench.parse_args([]).batch is None
+    assert bench.parse_args(["--config", "c4", "--batch", "4"]).batch == 4

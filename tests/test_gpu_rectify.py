@@ -203,6 +203,46 @@ def test_class_path_back_to_back_on_a_side_stream(cfg):
     check(lib().sdr_sgbm_set_stream(left._h, ctypes.c_void_p(s0.cuda_stream)))
 
 
+def test_live_loop_six_frames_in_flight(cfg):
+    """bench.py's C4 default: six LiveLoop slots (own matchers and filter, one shared rectifier)
+    on six streams, frames issued round-robin with no host synchronisation and every slot reused
+    while the others run -- each frame's filtered disparity and depth must equal the same frame
+    run alone."""
+    from stereo_depth_ruler_amd.pipeline import LiveLoop
+
+    dev = torch.device("cuda", 0)
+    r = StereoRectifier(cfg)
+    ns, nf = 6, 14
+    frames = [torch.from_numpy(sbs_frames(1, seed=500 + i)).to(dev) for i in range(nf)]
+    s0 = torch.cuda.current_stream(dev)
+    solo = LiveLoop(r, cfg.Q, 1)
+    ref = []
+    for fr in frames:
+        solo.enqueue(fr, s0)
+        ref.append((solo.filtered.clone(), solo.depth.clone()))
+        torch.cuda.synchronize()
+    solo.close()
+    pipes = [LiveLoop(r, cfg.Q, 1) for _ in range(ns)]
+    streams = [s0] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+    got = [None] * nf
+    for i, fr in enumerate(frames):
+        k = i % ns
+        with torch.cuda.stream(streams[k]):
+            pipes[k].enqueue(fr, streams[k])
+            # (copied on the slot's stream, before its next frame overwrites the buffers)
+            got[i] = (pipes[k].filtered.clone(), pipes[k].depth.clone())
+    torch.cuda.synchronize()
+    for i in range(nf):
+        assert torch.equal(got[i][0], ref[i][0]), f"frame {i}: filtered disparity"
+        assert torch.equal(got[i][1].view(torch.int32), ref[i][1].view(torch.int32)), f"frame {i}: depth"
+    for p in pipes:
+        p.close()
+    # the shared rectifier is left on one of these streams: back to its own before they go
+    from stereo_depth_ruler_amd._lib import check, lib
+
+    check(lib().sdr_rectifier_reset_stream(r._h))
+
+
 def test_live_loop_with_display_outputs(oracle, cfg):
     """pipeline.LiveLoop(display=True): the reference's whole per-frame loop body
     (stereo_displayer.cpp:155-173) for a batch of 3 frames -- rectify, computeDisparity,

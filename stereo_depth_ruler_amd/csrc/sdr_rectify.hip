@@ -117,6 +117,42 @@ __global__ __launch_bounds__(256) void k_remap(const uint8_t* __restrict__ src, 
     for (int c = 0; c < CN; c++) d[c] = (uint8_t)v[c];
 }
 
+// remap_px<3> with each source row's two taps fetched as one 6-byte span (a dword and a short at
+// byte 3 * cx, cx = clamp(sx, 0, sw - 2): both taps of an interior pixel, and every valid tap of
+// an edge one, lie inside it, and it never leaves the row) instead of six byte loads; a tap's
+// bytes are picked by its position in the span, invalid taps masked as before.  Needs sw >= 2.
+__device__ __forceinline__ uint64_t bgr_span(const uint8_t* p) {
+    uint32_t lo;
+    uint16_t hi;
+    __builtin_memcpy(&lo, p, 4);
+    __builtin_memcpy(&hi, p + 4, 2);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ void remap_px_bgr_span(const uint8_t* __restrict__ src, int sw, int sh, size_t sstride,
+                                                  uint32_t m1, uint32_t m2, int* out) {
+    const int sx = (int)(int16_t)(m1 & 0xffff), sy = (int)(int16_t)(m1 >> 16);
+    const int ax = (int)(m2 & 31), ay = (int)(m2 >> 5) & 31;
+    const int w00 = (32 - ax) * (32 - ay) * 32, w01 = ax * (32 - ay) * 32;
+    const int w10 = (32 - ax) * ay * 32, w11 = ax * ay * 32;
+    const bool x0 = sx >= 0 && sx < sw, x1 = sx + 1 >= 0 && sx + 1 < sw;
+    const bool y0 = sy >= 0 && sy < sh, y1 = sy + 1 >= 0 && sy + 1 < sh;
+    const int cx = min(max(sx, 0), sw - 2);
+    const int cy0 = min(max(sy, 0), sh - 1), cy1 = min(max(sy + 1, 0), sh - 1);
+    const uint64_t s0 = bgr_span(src + (size_t)cy0 * sstride + 3 * cx);
+    const uint64_t s1 = bgr_span(src + (size_t)cy1 * sstride + 3 * cx);
+    // bit offsets of the two taps in the span (a masked tap's offset is any valid one)
+    const int b0 = 24 * min(max(sx - cx, 0), 1), b1 = 24 * min(max(sx + 1 - cx, 0), 1);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const int v00 = (x0 && y0) ? (int)((s0 >> (b0 + 8 * c)) & 0xff) : 0;
+        const int v01 = (x1 && y0) ? (int)((s0 >> (b1 + 8 * c)) & 0xff) : 0;
+        const int v10 = (x0 && y1) ? (int)((s1 >> (b0 + 8 * c)) & 0xff) : 0;
+        const int v11 = (x1 && y1) ? (int)((s1 >> (b1 + 8 * c)) & 0xff) : 0;
+        const int acc = v00 * w00 + v01 * w01 + v10 * w10 + v11 * w11;
+        out[c] = min(max((acc + (1 << 14)) >> 15, 0), 255);
+    }
+}
+
 __device__ __forceinline__ int bgr2gray(int b, int g, int r) {
     return (b * 1868 + g * 9617 + r * 4899 + (1 << 13)) >> 14;
 }
@@ -155,7 +191,7 @@ __global__ __launch_bounds__(256) void k_sbs_ingest(SbsArgs a) {
     }
     int v[4][3];
 #pragma unroll
-    for (int q = 0; q < 4; q++) remap_px<3>(src, W, H, a.sstride, e1[q], e2[q], v[q]);
+    for (int q = 0; q < 4; q++) remap_px_bgr_span(src, W, H, a.sstride, e1[q], e2[q], v[q]);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int x = 2 * x2 + (q & 1), y = 2 * y2 + (q >> 1);
@@ -400,6 +436,7 @@ int sdr_rectify_sbs_device(sdr_rectifier* h, const uint8_t* d_sbs, size_t sbs_st
         return sdr::set_error(SDR_ERR_ARG, "bad SBS stride (frame must be (2*W) x H BGR)");
     if ((d_small_left || d_small_right) && ((h->W & 1) || (h->H & 1)))
         return sdr::set_error(SDR_ERR_SIZE, "INTER_AREA 0.5x needs even width and height");
+    if (h->W < 2) return sdr::set_error(SDR_ERR_SIZE, "the SBS ingest needs eyes at least 2 pixels wide");
     RECT_HIP(hipSetDevice(h->device));
     sdr::SbsArgs a{};
     a.sbs = d_sbs;

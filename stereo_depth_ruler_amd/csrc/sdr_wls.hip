@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_transpose2(const float* __restrict__ s0
 //      row, so the row's right map is all it needs): full-size confidence x255, A = conf * d,
 //      B = conf (ROI-compact)
 //   4. the row's FGS weights from the guide (Ch row-major for k_fgs_pcr or column-major for the
-//      sequential sweep, Cv row-major)
+//      sequential sweep, Cv row-major), computed in step 1's column loop
 // Rows outside the ROI only get the confidence map's 255.  Dynamic LDS: 32 B per ROI column
 // (int64 + int32 column sums and a float discontinuity value, per map).
 template <int RMAX>
@@ -1089,12 +1089,27 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
 #pragma unroll
     for (int t = 0; t <= 2 * RMAX; t++)
         rowo[t] = (size_t)(g.ry + reflect101(i + min(max(t - RMAX, -r), r), g.rh)) * g.W;
+    // the row's FGS weights from the guide (k_fgs_weights' formulas; the sequential solver's
+    // layouts: Ch at j*hp + i, Cv at i*wp + j, fgs_pad4), computed in the first phase's column loop
+    // so that their loads share its round trips
+    const uint8_t* gr = guide + (size_t)f * gfstride + (size_t)(g.ry + i) * gstride + g.rx;
+    const int wp = ch_rowmajor ? rw : fgs_pad4(rw), hp = ch_rowmajor ? g.rh : fgs_pad4(g.rh);
+    const size_t wfo = (size_t)f * wp * hp;
+    const int gs = i + 1 < g.rh ? (int)gstride : 0;
     for (int j = tid; j < rw; j += T) {
         int vl[2 * RMAX + 1], vr[2 * RMAX + 1];
+        const int gv = gr[j], gh = gr[min(j + 1, rw - 1)], gd = gr[gs + j];
 #pragma unroll
         for (int t = 0; t <= 2 * RMAX; t++) {
             vl[t] = L[rowo[t] + g.rx + j];
             vr[t] = R[rowo[t] + g.rrx + j];
+        }
+        {
+            // (unconditional lookups from clamped neighbours, then the edges' zeros)
+            const int dh = gv - gh, dv = gv - gd;
+            const float ch = lut[dh * dh], cv = lut[dv * dv];
+            ChW[wfo + (ch_rowmajor ? (size_t)i * rw + j : (size_t)j * hp + i)] = j + 1 < rw ? ch : 0.0f;
+            Cv[wfo + (size_t)i * wp + j] = gs ? cv : 0.0f;
         }
         int s0 = 0, s1 = 0;
         int64_t q0 = 0, q1 = 0;
@@ -1170,25 +1185,7 @@ __global__ __launch_bounds__(256) void k_wls_prep(const int16_t* __restrict__ dl
             }
         }
     }
-    // FGS weights of the guide's ROI row i (k_fgs_weights' formulas)
-    const uint8_t* gr = guide + (size_t)f * gfstride + (size_t)(g.ry + i) * gstride + g.rx;
-    // (the sequential solver's layouts: Ch at j*hp + i, Cv at i*wp + j; fgs_pad4)
-    const int wp = ch_rowmajor ? rw : fgs_pad4(rw), hp = ch_rowmajor ? g.rh : fgs_pad4(g.rh);
-    const size_t wfo = (size_t)f * wp * hp;
-    for (int j = tid; j < rw; j += T) {
-        const int v = gr[j];
-        float ch = 0.0f, cv = 0.0f;
-        if (j + 1 < rw) {
-            const int d = v - gr[j + 1];
-            ch = lut[d * d];
-        }
-        if (i + 1 < g.rh) {
-            const int d = v - gr[gstride + j];
-            cv = lut[d * d];
-        }
-        ChW[wfo + (ch_rowmajor ? (size_t)i * rw + j : (size_t)j * hp + i)] = ch;
-        Cv[wfo + (size_t)i * wp + j] = cv;
-    }
+
 }
 
 // saturate_cast<short>(float): round half to even, saturate; 0 where FGS(conf) == 0 (cv::divide

@@ -60,10 +60,24 @@ __global__ __launch_bounds__(256) void k_prefilter(const uint8_t* __restrict__ L
         const uint8_t* gn = y > 0 ? gr - stride : gr;
         const uint8_t* gs = y < H - 1 ? gr + stride : gr;
         uint8_t* rows = (uint8_t*)(q6 + W);
-        for (int x = threadIdx.x; x < WB; x += blockDim.x) {
-            rows[x] = gn[x];
-            rows[WB + x] = gr[x];
-            rows[2 * WB + x] = gs[x];
+        if (((WB | (int)stride | (int)fstride | (int)(uintptr_t)base) & 3) == 0) {
+            // dword-aligned rows (the class path's half-size images, typical frames): four bytes a
+            // lane, the three rows' loads issued together (the LDS rows start 8-byte aligned and
+            // are WB apart, a multiple of 4)
+            uint32_t* rw = (uint32_t*)rows;
+            const int nw = WB >> 2;
+            for (int x = threadIdx.x; x < nw; x += blockDim.x) {
+                const uint32_t a = ((const uint32_t*)gn)[x], b = ((const uint32_t*)gr)[x], c = ((const uint32_t*)gs)[x];
+                rw[x] = a;
+                rw[nw + x] = b;
+                rw[2 * nw + x] = c;
+            }
+        } else {
+            for (int x = threadIdx.x; x < WB; x += blockDim.x) {
+                rows[x] = gn[x];
+                rows[WB + x] = gr[x];
+                rows[2 * WB + x] = gs[x];
+            }
         }
         __syncthreads();
     }

@@ -1,8 +1,8 @@
 #!/bin/bash
-# the GPU suite, smoke, and the C4 line on one stream and at its default 6 (after a class-path change)
+# after a class-path change: the GPU suite, smoke, and the C4 line on one stream and at its default 6
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/check_fork
+O=gpurun_out/check_c4
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $O/tests.log 2>&1 &&
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 &&

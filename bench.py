@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "stereo Mpix/s (disparity+reproject) at 1280×720 d=128, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md chip table: max clock (the latency floors' cycles -> time)
 
 # name -> (description, W, H, SGBM args (create order), batch, reproject handleMissing, kind)
 #   kind "sgbm":  rectified gray pairs -> compute + /16 + reprojectImageTo3D (pcd_write.cpp:111-116)
@@ -102,6 +103,12 @@ def cpu_baseline(cfg, seconds_target=15.0):
     from oracle import oracle as O
     from stereo_depth_ruler_amd import synthetic as S
 
+    # the restatement built -O3 -march=native, compiled here on the host that times it
+    try:
+        build_flags = O.select_build("native")
+        O.lib()
+    except Exception as e:  # no compiler on this host: the shipped portable build
+        build_flags = O.select_build("portable") + f" (native build failed: {type(e).__name__})"
     _, W, H, args, _, hm, kind = cfg
     model, ncpu = host_cpu()
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
@@ -177,6 +184,7 @@ def cpu_baseline(cfg, seconds_target=15.0):
                     "unit": "Mpix/s", "threads": 1, "frames": len(lat)},
         "host": {"cpu_model": model, "nproc": ncpu, "threads_used": threads,
                  "omp_num_threads": omp or None, "policy": policy},
+        "build": build_flags,
     }
 
 
@@ -200,8 +208,10 @@ def stream_probe(dev, mib=2048, iters=20):
 
     g = ctypes.c_double()
     check(lib().sdr_stream_probe(dev.index, mib << 20, iters, ctypes.byref(g)))
-    return {"gbs": round(g.value, 1), "what": f"sdr_stream_probe: {iters} copies of {mib} MiB (16-B loads, "
-                                              f"non-temporal stores), read + write bytes"}
+    return {"gbs": round(g.value, 1), "what": f"sdr_stream_probe: the fastest of 12 copy variants (4 or 8 "
+                                              f"16-B loads in flight per thread, plain or non-temporal "
+                                              f"stores, 4/8/16 workgroups a CU), {iters} copies of {mib} MiB "
+                                              f"each, read + write bytes"}
 
 
 def free_port() -> int:
@@ -263,6 +273,9 @@ def parse_args(argv=None):
     ap.add_argument("--stream-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="time a 2 GiB device copy after the run (roofline.stream_probe: this box's "
                          "streaming rate beside the dominant kernel's)")
+    ap.add_argument("--hbm-only", action=argparse.BooleanOptionalAction, default=True,
+                    help="C2: also time k_paths over a 4-frame batch whose cost volume exceeds the "
+                         "Infinity Cache (roofline.hbm_only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses the N>1 path with every "
                          "rank on the one GPU of a 1-GPU box (gather staged through host memory)")
@@ -544,6 +557,7 @@ def main():
                 for name, (ms, c) in corr.items() if c}
         if not per_kind["k_paths"][1]:
             return kern, None
+        fgs = fgs_model(per_kind, corr, all_corr, steps) if kind == "live" else None
         # algorithmic bytes per launch of the path kernels (2 B per int16 cell):
         #   k_paths: each of its directions reads C and writes its own record;
         #   k_sweep (batched MODE_HH, up: N, NE, NW) and k_sweep_down (SE, SW): one pass reads C
@@ -566,8 +580,11 @@ def main():
         name = max((n for n in models if per_kind[n][1]), key=lambda n: corr[n][0])
         tot_ms, cnt = corr[name]
         bytes_per_launch, model = models[name]
-        avg_s = tot_ms / cnt / 1e3
+        # the primary figure is the raw event-timed duration (the per-launch event
+        # overhead is not uniform across kernels, so the corrected time is kept as an estimate)
+        avg_s = per_kind[name][0] / cnt / 1e3
         achieved = bytes_per_launch / avg_s / 1e9
+        avg_s_corr = tot_ms / cnt / 1e3
         label = {
             "k_paths": f"k_paths<DPL={2 if D <= 128 else 4}> or k_paths_tc (two chains per wave, the engine's pick "
                        f"for latency-bound launches) ({kp_dirs} of the {P} path directions of a batch in "
@@ -587,7 +604,8 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "bytes_model": f"{model}; cells={'2 matchers*' if nmatch == 2 else ''}batch*H*W1*D={cells}",
             "avg_launch_us": round(avg_s * 1e6, 2),
-            "avg_launch_us_events": round(per_kind[name][0] / cnt * 1e3, 2),
+            "avg_launch_us_overhead_corrected": round(avg_s_corr * 1e6, 2),
+            "achieved_overhead_corrected": round(bytes_per_launch / avg_s_corr / 1e9, 1),
             "event_overhead_us_per_launch": round(ovh_us, 2),
             "launches_timed": cnt,
             "kernel_share_of_gpu_time": round(tot_ms / all_corr, 4) if all_corr else None,
@@ -610,7 +628,55 @@ def main():
             "achieved": round(pipe_bytes / gpu_s / 1e9, 1),
             "frac": round(pipe_bytes / gpu_s / 1e9 / HBM_PEAK_GBS, 4),
         }
+        if fgs is not None and fgs["share_of_gpu_time"] > roof["kernel_share_of_gpu_time"]:
+            # the class path's frame: the sequential FGS passes, not a path kernel, take the most
+            # time; the line names them with their latency model, the HBM-bound path kernel beside
+            fgs["hbm_path_kernel"] = roof
+            roof = fgs
         return kern, roof
+
+    def fgs_model(per_kind, corr, all_corr, steps):
+        """The class path's sequential FGS passes (k_fgs_th, SDR_FGS_THOMAS: ximgproc's order) as a
+        latency-bound kernel.  A pass solves every line of the WLS ROI (rows: rh lines of rw
+        samples, columns: rw lines of rh) with one lane per line: each line is a chain of rw (or rh)
+        forward steps then as many back steps, each step a dependent sequence of packed-f32 ops --
+        5 forward (the right-hand sides' elimination from the precomputed coefficients: mul, the
+        Markstein correction fma, fma, and the two-image pack), 2 back (fma, mul) -- at 8.4 cycles
+        a dependent op on one wave (profiles/r5_probe_fgs_step.txt).  floor = the chain's
+        dependent-op cycles at the peak clock; frac = floor / measured pass time."""
+        tot, cnt = per_kind["fgs_pass"]
+        if not cnt:
+            return None
+        roi = pipes[0].wls.getROI(Wm, Hm)
+        rw, rh = roi[2], roi[3]
+        # the passes alternate rows and columns (3 iterations: 3 + 3 per frame)
+        chain = (rw + rh) / 2.0
+        cyc_op, fwd_ops, back_ops = 8.4, 5, 2
+        floor_us = chain * (fwd_ops + back_ops) * cyc_op / (CLOCK_GHZ * 1e3)
+        avg_us = tot / cnt * 1e3
+        samples = nmatch // 2 * batch * rw * rh  # line-samples one pass solves (both images together)
+        coef = per_kind["fgs_coef"]
+        return {
+            "bound": "latency",
+            "kernel": "k_fgs_th (sequential FGS pass, SDR_FGS_THOMAS: one lane per line, the solver wave "
+                      "reads only LDS, DMA loader waves and a writer wave beside it)",
+            "achieved": round(samples / (avg_us * 1e-6) / 1e9, 3),
+            "peak": round(samples / (floor_us * 1e-6) / 1e9, 3),
+            "unit": "G line-samples/s",
+            "frac": round(floor_us / avg_us, 4),
+            "traffic": None,
+            "model": (f"a pass = lines of a {rw}x{rh} ROI, mean chain {chain:.0f} samples (rows {rw}, columns "
+                      f"{rh}); floor = chain x ({fwd_ops} fwd + {back_ops} back dependent ops) x {cyc_op} "
+                      f"cycles at {CLOCK_GHZ} GHz = {floor_us:.2f} us a pass"),
+            "avg_launch_us": round(avg_us, 2),
+            "floor_us": round(floor_us, 2),
+            "measured_cycles_per_sample": round(avg_us * CLOCK_GHZ * 1e3 / chain, 1),
+            "floor_cycles_per_sample": round((fwd_ops + back_ops) * cyc_op, 1),
+            "launches_timed": cnt,
+            "passes_per_frame": cnt / max(1, steps) / max(1, batch),
+            "coef_jobs_us_per_launch": round(coef[0] / coef[1] * 1e3, 2) if coef[1] else None,
+            "share_of_gpu_time": round((corr["fgs_pass"][0] + corr["fgs_coef"][0]) / all_corr, 4) if all_corr else 0,
+        }
 
     roofline = None
     kernels = None
@@ -641,6 +707,35 @@ def main():
                         run(j, 0, 0)
             return ingest
 
+        def hbm_only_paths(frames=4, reps=5):
+            """k_paths with a cost volume the 256 MiB Infinity Cache cannot hold:
+            the same C2 launch shape over `frames` frames in one batch (C = frames x 212 MB), so its
+            four re-reads of C come from HBM, not the cache; one matcher, single stream, event-timed
+            (raw durations, no overhead correction)."""
+            mm = sdr.StereoSGBM.create(*args, device=dev.index)
+            f = min(frames, nf)
+            dd = torch.empty((f, H, W), dtype=torch.int16, device=dev)
+            xx = torch.empty((f, H, W, 3), dtype=torch.float32, device=dev)
+            with torch.cuda.stream(streams[0]):
+                mm.compute_reproject(Ld[:f], Rd[:f], S.REFERENCE_Q, hm, disp=dd, xyz=xx)  # warm, allocate
+                torch.cuda.synchronize()
+                mm.enable_timing(2)
+                mm.kernel_time(-1, reset=True)
+                for _ in range(reps):
+                    mm.compute_reproject(Ld[:f], Rd[:f], S.REFERENCE_Q, hm, disp=dd, xyz=xx)
+            torch.cuda.synchronize()
+            ms_, c = mm.kernel_time(_sg.KERNEL_PATHS, reset=True)
+            mm.close()
+            cells_f = f * H * w1 * D
+            b = cells_f * 4 * (P - 1)
+            us = ms_ / c * 1e3
+            return {"kernel": "k_paths (the C2 launch shape)", "frames_per_launch": f,
+                    "cost_volume_MB": round(cells_f * 2 / 1e6, 1), "algorithmic_bytes_per_launch": b,
+                    "avg_launch_us": round(us, 2), "launches": c, "achieved": round(b / us / 1e3, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(b / us / 1e3 / HBM_PEAK_GBS, 4),
+                    "note": "C beyond the Infinity Cache: the fraction of HBM itself; the main roofline's "
+                            "batch-1 C (212 MB) is partly re-read from the 256 MiB cache"}
+
         # the same single-stream steps without events first: the step time the per-kernel table
         # is reconciled with (kernel_report's step_us)
         torch.cuda.synchronize()
@@ -664,8 +759,12 @@ def main():
             if inflight is not None:
                 roofline["in_flight"] = inflight
             if a.stream_probe:
-                roofline["stream_probe"] = stream_probe(dev)
-                roofline["frac_of_probe"] = round(roofline["achieved"] / roofline["stream_probe"]["gbs"], 4)
+                probe = stream_probe(dev)
+                hb = roofline.get("hbm_path_kernel", roofline)
+                hb["stream_probe"] = probe
+                hb["frac_of_probe"] = round(hb["achieved"] / probe["gbs"], 4)
+            if a.hbm_only and kind == "sgbm" and mode == 0:
+                roofline["hbm_only"] = hbm_only_paths()
         m.enable_timing(0)
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6

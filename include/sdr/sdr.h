@@ -86,15 +86,21 @@ int sdr_sgbm_set_params(sdr_sgbm* h, const sdr_sgbm_params* p);
 int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p);
 /* HIP stream (hipStream_t) the handle launches on (NULL = the HIP null stream, e.g. torch's
  * default stream); a new handle uses a stream of its own, restored by sdr_sgbm_reset_stream.
- * Changing the stream orders the handle's earlier work before the new stream's: an event is
- * recorded on the previous stream at the switch (not after every call: a record is a queue
- * barrier, ~6 us of idle queue per class-path frame).  So a caller's stream must outlive the
- * handle's use of it: move the handle off a stream (set another, or sdr_sgbm_reset_stream) before
- * destroying that stream, and destroy the handle while its current stream exists.  HIP does not
- * validate a destroyed stream's handle -- an event recorded on one, or waited on after it was
- * recorded there, crashes the process (MI355X, ROCm 7.2, round 5) -- so the engine cannot detect
- * a violation; tests/test_gpu_streams.py exercises the supported order. */
+ * Changing the stream orders the handle's earlier work before the new stream's.
+ * sdr_sgbm_set_stream binds a TRANSIENT stream: the caller may destroy it as soon as the calls
+ * made on it have returned (and its work is done, as hipStreamDestroy requires); the handle
+ * never touches it afterwards -- at the end of every call on it the handle records an event
+ * there and relays it through its own stream, which later switches, sdr_sgbm_last_status and
+ * sdr_sgbm_destroy use instead.  The next call must follow a set_stream / reset_stream naming a
+ * live stream.
+ * sdr_sgbm_set_stream_ex(.., SDR_STREAM_PERSISTENT) binds a stream that outlives the handle's use
+ * of it (a pooled stream such as torch's, or one the caller keeps until it has moved the handle
+ * off it): no event is recorded per call, only at the next switch (an event record is a queue
+ * barrier: ~6 us of idle queue per class-path frame when recorded after every call).  The
+ * Python layer passes the flag for torch's pooled and default streams, not for external ones. */
+enum { SDR_STREAM_PERSISTENT = 1 };
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream);
+int sdr_sgbm_set_stream_ex(sdr_sgbm* h, void* stream, int flags);
 int sdr_sgbm_reset_stream(sdr_sgbm* h);
 void* sdr_sgbm_get_stream(const sdr_sgbm* h);
 
@@ -413,7 +419,9 @@ int sdr_sgbm_kernel_time(sdr_sgbm* h, int kind, int reset, float* total_ms, int*
  * that this process has the device to itself (sweeps of one process are ordered among themselves).
  * If a wait still gives up (another process's persistent kernel holding CUs for about a second),
  * that batch's output frames are written as INVALID ((minDisparity-1)*16, the reprojection's
- * frame minima too) and this call returns SDR_ERR_DEVICE once, then SDR_OK again.  The
+ * frame minima too) and SDR_ERR_DEVICE is returned once for the timeouts seen since the last
+ * report -- by this call, or by the next compute call if it sees them first -- then SDR_OK again
+ * (the device keeps a count, so copies of it still in flight cannot report a timeout twice).  The
  * host-pointer entry points compute one frame and never take the sweeps. */
 int sdr_sgbm_last_status(sdr_sgbm* h);
 /* Test hooks.  SDR_DEBUG_SWEEP_SPIN: polls a sweep's neighbour wait makes before it gives up

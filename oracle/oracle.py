@@ -34,11 +34,29 @@ _SOURCES = ("sgbm_oracle.c", "sgbm_oracle.h", "wls_oracle.c", "wls_oracle.h", "r
             "Makefile")
 
 
+_MAKE_TARGET = "all"
+# the builds of the same sources: portable (-march=x86-64-v2, the parity checker; built here and
+# shipped) and native (-march=native, the CPU baseline's; built on the host that times it)
+BUILDS = {"portable": ("_build", "all", "gcc -O3 -march=x86-64-v2 -ffp-contract=off"),
+          "native": ("_build_native", "native", "gcc -O3 -march=native -ffp-contract=off")}
+
+
+def select_build(kind: str) -> str:
+    """Chooses which build lib() loads (before its first call); returns the compile line."""
+    global _LIB_PATH, _MAKE_TARGET
+    d, target, flags = BUILDS[kind]
+    path = os.path.join(_HERE, d, "liboracle.so")
+    if _lib is not None and path != _LIB_PATH:
+        raise RuntimeError(f"the oracle is already loaded from {_LIB_PATH}")
+    _LIB_PATH, _MAKE_TARGET = path, target
+    return flags
+
+
 def build(force: bool = False) -> str:
     stale = not os.path.exists(_LIB_PATH) or any(
         os.path.getmtime(os.path.join(_HERE, f)) > os.path.getmtime(_LIB_PATH) for f in _SOURCES)
     if force or stale:
-        subprocess.check_call(["make", "-s", "-C", _HERE])
+        subprocess.check_call(["make", "-s", "-C", _HERE, _MAKE_TARGET])
     return _LIB_PATH
 
 

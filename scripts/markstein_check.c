@@ -2,12 +2,14 @@
  *   q0 = x * r,  rem = -fma(q0, den, -x),  q = fma(rem, r, q0)      (r = 1/den, correctly rounded)
  * against the IEEE quotient x / den, for den >= 1 (every FGS pivot is) and |q0| >= 2^-96 (the
  * kernel redoes a chunk with real divisions when some 0 < |q0| < 2^-96).  Random den over
- * [1, 2^60), random x of either sign (subnormals included) with |x / den| from 2^-150 to 2^100;
+ * [1, 2^102) (every pivot the accepted lambdas reach: den <= 1 + 2 lambda, lambda <= 2^100), random x of either sign (subnormals included) with |x / den| from 2^-150 to 2^100;
  * counts, separately, the mismatches below the threshold (the inputs the redo exists for).
- * Optional second argument: the threshold's exponent (default -96).
+ * Optional second argument: the threshold's exponent (default -96); third: den's exponent range
+ * (default 102; round 5 checked 60).
  *   gcc -O2 -mfma -o /tmp/markstein scripts/markstein_check.c -lm && /tmp/markstein 2000000000
  * (-mfma: fmaf must be the fused instruction; x86-64 with FMA3.)  Round 5 result: no mismatch at
- * or above the threshold in 2e9 pairs (x from the subnormal range up, zeros of both signs). */
+ * or above the threshold in 2e9 pairs with den < 2^60 (x from the subnormal range up, zeros of both
+ * signs); round 6 the same over den < 2^102: profiles/r6_markstein_check.txt. */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -35,9 +37,10 @@ static inline uint32_t ubits(float f) {
 int main(int argc, char** argv) {
     const long n = argc > 1 ? atol(argv[1]) : 100000000L;
     const float thr = argc > 2 ? ldexpf(1.0f, atoi(argv[2])) : 0x1p-96f;  /* the redo threshold */
+    const int dmax = argc > 3 ? atoi(argv[3]) : 102;
     long bad = 0, below = 0, below_bad = 0;
     for (long i = 0; i < n; i++) {
-        const int de = (int)(rnd() % 60);                     /* den in [2^de, 2^(de+1)) */
+        const int de = (int)(rnd() % (uint64_t)dmax);         /* den in [2^de, 2^(de+1)) */
         const float den = fbits((uint32_t)(127 + de) << 23 | (uint32_t)(rnd() & 0x7fffff));
         const int qe = -150 + (int)(rnd() % 250);             /* |x / den| ~ 2^qe */
         const int xe = qe + de;

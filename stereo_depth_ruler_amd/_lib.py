@@ -75,6 +75,7 @@ SIGNATURES = [
     ("sdr_sgbm_set_params", _i, [_vp, _PP]),
     ("sdr_sgbm_get_params", _i, [_vp, _PP]),
     ("sdr_sgbm_set_stream", _i, [_vp, _vp]),
+    ("sdr_sgbm_set_stream_ex", _i, [_vp, _vp, _i]),
     ("sdr_sgbm_reset_stream", _i, [_vp]),
     ("sdr_sgbm_get_stream", _vp, [_vp]),
     ("sdr_sgbm_compute", _i, [_vp, _vp, _vp, _i, _i, _i, _sz, _vp, _sz]),

@@ -345,7 +345,18 @@ struct sdr_sgbm {
     // recorded after the last kernel that touches this handle's scratch; a stream switch makes
     // the new stream wait for it, so one matcher used from two streams never overlaps itself
     hipEvent_t done = nullptr;
-    bool pending = false;  // work enqueued since the last switch, not yet recorded
+    bool pending = false;  // work enqueued on a persistent stream since the last switch, not yet recorded
+    // the current stream outlives the handle's use of it: the handle's own stream, or a caller's
+    // stream declared persistent (sdr_sgbm_set_stream_ex).  Only such a stream is touched after
+    // the call that used it has returned (the lazy retire record at a switch, destroy's sync).
+    bool persistent = true;
+    // `done` was recorded after the handle's last call on a transient stream, relayed through the
+    // handle's own stream so that it refers to no caller stream: the next stream waits on it
+    bool relayed = false;
+    bool needs_wait = false;  // the current stream has not waited on `done` yet (begin_call)
+    // sweep timeouts reported so far (the device word counts them; its copy, status_host, is
+    // refreshed after every sweep batch)
+    int status_reported = 0;
     // the last compute skipped the no-op LR check (disp12MaxDiff >= D): debug stage 2 is then
     // rebuilt on request from the WTA map with this geometry
     bool lr_skipped = false;
@@ -368,32 +379,80 @@ bool capturing(hipStream_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
-// The handle's last enqueue, for the next stream that uses its scratch (h->done).  Recorded lazily:
-// only when the handle moves to another stream does its old stream get the event (after everything
-// queued there so far, the handle's work included), and the new stream wait on it.  An event record
-// is a queue barrier: recorded after every call it left a ~6 us idle gap per class-path frame
-// (rounds 4 and 5).  Hence the previous stream must still exist when the handle changes streams,
-// as it must for sdr_sgbm_destroy's synchronisation (sdr.h: HIP does not validate a destroyed
-// stream, so this is the caller's contract, as for any library handle bound to a stream).  Nothing
-// is recorded into or waited on from a graph capture: the capture's replays order themselves.
-hipError_t retire(sdr_sgbm* h) {
-    h->pending = true;
-    return hipSuccess;
+// The handle's last enqueue, for the next stream that uses its scratch (h->done).
+//  * On a persistent stream (the handle's own, or a caller's declared so: torch's pooled streams)
+//    the record is lazy: only when the handle moves to another stream does its old stream get the
+//    event (after everything queued there so far, the handle's work included), and the new stream
+//    wait on it.  An event record is a queue barrier: recorded after every call it left a ~6 us
+//    idle gap per class-path frame (rounds 4 and 5).
+//  * On a transient caller stream (sdr_sgbm_set_stream; the caller may destroy it as soon as its
+//    work is done) the event is recorded at the end of every call, and relayed through the
+//    handle's own stream (that stream waits on it, then the event is recorded again there), so
+//    neither a later switch nor destroy touches the caller's stream: HIP does not validate a
+//    destroyed stream's handle, and an event whose last record was on one crashes a later wait
+//    (round 5, gpurun_out/r5b/tests.log).
+// Nothing is recorded into or waited on from a graph capture: the capture's replays order
+// themselves.
+// `done` after everything queued on `from`, re-recorded on the handle's own stream
+hipError_t relay(sdr_sgbm* h, hipStream_t from) {
+    hipError_t e = hipEventRecord(h->done, from);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->own_stream, h->done, 0);
+    if (e == hipSuccess) e = hipEventRecord(h->done, h->own_stream);
+    h->relayed = e == hipSuccess;
+    return e;
 }
-int use_stream(sdr_sgbm* h, hipStream_t s) {
+hipError_t retire(sdr_sgbm* h) {
+    if (h->persistent) {
+        h->pending = true;
+        return hipSuccess;
+    }
+    if (!h->done || capturing(h->stream)) return hipSuccess;
+    return relay(h, h->stream);
+}
+// At the start of a call: the handle's stream waits for work the handle queued elsewhere and
+// has not been ordered before it yet (the class path's unpaired right matcher, run on a side stream)
+hipError_t begin_call(sdr_sgbm* h) {
+    if (!h->needs_wait) return hipSuccess;
+    h->needs_wait = false;
+    if (capturing(h->stream)) return hipSuccess;
+    return hipStreamWaitEvent(h->stream, h->done, 0);
+}
+int use_stream(sdr_sgbm* h, hipStream_t s, bool persistent) {
     // a stream being captured neither queries nor waits on an event recorded outside the capture
     // (both invalidate a global-mode capture); torch.cuda.graph synchronises before it captures,
     // and a caller capturing by hand orders the handle's earlier work before the capture itself
-    if (s == h->stream) return SDR_OK;
-    hipError_t e = hipSuccess;
-    if (h->pending && h->done && !capturing(h->stream) && !capturing(s)) {
-        e = hipEventRecord(h->done, h->stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(s, h->done, 0);
+    persistent = persistent || s == h->own_stream;
+    if (s == h->stream) {
+        // the same stream, now declared transient: record what the persistent form left pending
+        // (the stream exists: this call names it)
+        hipError_t e = hipSuccess;
+        if (h->persistent && !persistent && h->pending) {
+            h->persistent = false;
+            h->pending = false;
+            e = retire(h);
+        }
+        h->persistent = persistent;
+        if (e != hipSuccess)
+            return fail(SDR_ERR_DEVICE, std::string("ordering the handle's work on its stream: ") + hipGetErrorString(e));
+        return SDR_OK;
     }
+    hipError_t e = hipSuccess;
+    bool wait = false;
+    if (h->pending && h->done && !capturing(h->stream) && !capturing(s)) {
+        // h->pending implies a persistent previous stream: it still exists
+        e = hipEventRecord(h->done, h->stream);
+        wait = true;
+    } else if (h->relayed && !capturing(s)) {
+        wait = true;  // recorded on the handle's own stream: no caller stream is touched
+    }
+    if (wait && e == hipSuccess) e = hipStreamWaitEvent(s, h->done, 0);
     // the handle moves to s even when the ordering failed: the error is reported once and the
     // handle stays usable on s
     h->pending = false;
+    h->relayed = false;
+    h->needs_wait = false;
     h->stream = s;
+    h->persistent = persistent;
     if (e != hipSuccess)
         return fail(SDR_ERR_DEVICE, std::string("ordering the handle's previous stream before the new one: ") +
                                         hipGetErrorString(e));
@@ -488,12 +547,13 @@ static int enqueue_compute(sdr_sgbm* h, const uint8_t* L, const uint8_t* R, int 
     // reported here, by the next call, if no sdr_sgbm_last_status has reported it yet.  The
     // host copy is refreshed asynchronously after every sweep batch, so this check never waits
     // (a timeout still in flight is reported by the call after)
-    if (h->status_host && __atomic_load_n(h->status_host, __ATOMIC_ACQUIRE)) {
-        __atomic_store_n(h->status_host, 0, __ATOMIC_RELEASE);
-        SDR_HIP(hipMemsetAsync(h->status.p, 0, sizeof(int), h->stream));
+    // (a count of timed-out batches: each is reported once, whatever copies are still in flight)
+    if (h->status_host && __atomic_load_n(h->status_host, __ATOMIC_ACQUIRE) != h->status_reported) {
+        h->status_reported = __atomic_load_n(h->status_host, __ATOMIC_ACQUIRE);
         return fail(SDR_ERR_DEVICE, "an earlier MODE_HH batch's row sweep timed out waiting for a neighbouring "
                                     "tile: that batch's frames were written as INVALID (this call did not run)");
     }
+    SDR_HIP(begin_call(h));
     Eff e;
     int rc = make_eff(h->p, W, H, &e);
     if (rc) return rc;
@@ -855,7 +915,8 @@ int sdr_sgbm_create(const sdr_sgbm_params* p, int device, sdr_sgbm** out) {
 int sdr_sgbm_destroy(sdr_sgbm* h) {
     if (!h) return SDR_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    // a transient caller stream is never touched after its call: the relay put its work on own_stream
+    if (h->stream && h->persistent) (void)hipStreamSynchronize(h->stream);
     if (h->own_stream && h->own_stream != h->stream) (void)hipStreamSynchronize(h->own_stream);
     if (h->status_host) (void)hipHostFree(h->status_host);
     for (Buf* b : {&h->sweep, &h->status, &h->planesL, &h->planesR, &h->sink, &h->C, &h->Lr, &h->Caux, &h->draw, &h->dlr, &h->dfin, &h->keys2,
@@ -892,13 +953,21 @@ int sdr_sgbm_get_params(const sdr_sgbm* h, sdr_sgbm_params* p) {
 int sdr_sgbm_set_stream(sdr_sgbm* h, void* stream) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
     (void)hipSetDevice(h->device);
-    return use_stream(h, (hipStream_t)stream);  // NULL = the HIP null (legacy default) stream
+    // NULL = the HIP null (legacy default) stream, which always exists
+    return use_stream(h, (hipStream_t)stream, stream == nullptr);
+}
+
+int sdr_sgbm_set_stream_ex(sdr_sgbm* h, void* stream, int flags) {
+    if (!h) return fail(SDR_ERR_ARG, "null handle");
+    if (flags & ~SDR_STREAM_PERSISTENT) return fail(SDR_ERR_ARG, "unknown stream flags");
+    (void)hipSetDevice(h->device);
+    return use_stream(h, (hipStream_t)stream, stream == nullptr || (flags & SDR_STREAM_PERSISTENT));
 }
 
 int sdr_sgbm_reset_stream(sdr_sgbm* h) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
     (void)hipSetDevice(h->device);
-    return use_stream(h, h->own_stream);
+    return use_stream(h, h->own_stream, true);
 }
 
 void* sdr_sgbm_get_stream(const sdr_sgbm* h) { return h ? (void*)h->stream : nullptr; }
@@ -1277,14 +1346,20 @@ static int class_enqueue(sdr_sgbm* left, sdr_sgbm* right, sdr_wls* wls, const ui
         }
         SDR_HIP(hipEventRecord(left->fork, st));
         SDR_HIP(hipStreamWaitEvent(left->side, left->fork, 0));
+        // the right matcher runs on the side stream and returns to its own stream binding without
+        // touching that stream now (a transient one may already be gone): its work is relayed
+        // through its own stream and its stream waits on it at its next call (begin_call)
         hipStream_t rs = right->stream;
-        if ((rc = use_stream(right, left->side))) return rc;
+        const bool rp = right->persistent;
+        if ((rc = use_stream(right, left->side, true))) return rc;
         rc = enqueue_compute(right, sr, sl, w2, h2, w2, px2, F, dr, nullptr, &fin);
-        const hipError_t re = retire(right);
-        const int rc2 = use_stream(right, rs);
+        const hipError_t re = relay(right, left->side);
+        right->pending = false;
+        right->stream = rs;
+        right->persistent = rp;
+        right->needs_wait = true;
         if (rc) return rc;
         SDR_HIP(re);
-        if (rc2) return rc2;
         SDR_HIP(hipEventRecord(left->join, left->side));
     }
     if (!paired) {
@@ -1401,12 +1476,11 @@ int sdr_sgbm_last_status(sdr_sgbm* h) {
     if (!h) return fail(SDR_ERR_ARG, "null handle");
     if (!h->status_host) return SDR_OK;  // no sweep batch has run on this handle
     SDR_HIP(hipSetDevice(h->device));
-    SDR_HIP(hipStreamSynchronize(h->stream));
-    if (!__atomic_load_n(h->status_host, __ATOMIC_ACQUIRE)) return SDR_OK;
-    // reported: clear the device word and its copy
-    SDR_HIP(hipMemsetAsync(h->status.p, 0, sizeof(int), h->stream));
-    SDR_HIP(hipStreamSynchronize(h->stream));
-    __atomic_store_n(h->status_host, 0, __ATOMIC_RELEASE);
+    if (h->persistent) SDR_HIP(hipStreamSynchronize(h->stream));
+    SDR_HIP(hipStreamSynchronize(h->own_stream));  // relayed work (transient streams, side stream)
+    const int n = __atomic_load_n(h->status_host, __ATOMIC_ACQUIRE);
+    if (n == h->status_reported) return SDR_OK;
+    h->status_reported = n;  // the device word counts timeouts and is never cleared
     return fail(SDR_ERR_DEVICE, "a MODE_HH row sweep timed out waiting for a neighbouring tile: that "
                                 "batch's frames were written as INVALID");
 }

@@ -669,15 +669,36 @@ __global__ void k_selftest(int* fails, uint32_t seed) {
     if (mu != e) atomicAdd(&fails[3], 1);
 }
 
-// The streaming probe (sdr_stream_probe): a grid-stride copy with 16-byte loads and non-temporal
-// stores -- k_paths' own data flow, one read and one write per byte of a cost row -- over buffers
-// larger than the caches, so a bench line can put the box's streaming rate beside its kernels'.
+// The streaming probe (sdr_stream_probe): the box's copy rate over buffers far larger than the
+// caches (2 GiB each way against the 256 MiB Infinity Cache), so a bench line can put the box's
+// streaming rate beside its kernels'.  Each thread moves U 16-byte vectors per trip, all U loads
+// issued before the first store (a one-load grid-stride loop keeps one load in flight per wave
+// and read 4.75-5.0 TB/s in round 5); a workgroup owns a contiguous span per trip, so its waves
+// sweep whole DRAM pages.  Variants: U = 4 / 8, plain or non-temporal stores, 4 / 8 / 16
+// workgroups a CU; the probe reports the fastest (the yardstick must reach the
+// guide's ~6.3 TB/s float4 copy for frac_of_probe to mean anything).
 typedef unsigned int probe_u32x4 __attribute__((ext_vector_type(4)));
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_stream_probe(const probe_u32x4* __restrict__ src,
                                                       probe_u32x4* __restrict__ dst, size_t n) {
-    const size_t nth = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nth)
-        __builtin_nontemporal_store(src[i], &dst[i]);
+    const size_t span = (size_t)256 * U;  // vectors a workgroup moves per trip
+    for (size_t base = (size_t)blockIdx.x * span; base < n; base += (size_t)gridDim.x * span) {
+        probe_u32x4 v[U];
+        if (base + span <= n) {
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(&src[base + u * 256 + threadIdx.x]);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (NT) __builtin_nontemporal_store(v[u], &dst[base + u * 256 + threadIdx.x]);
+                else dst[base + u * 256 + threadIdx.x] = v[u];
+            }
+        } else {
+            for (int u = 0; u < U; u++) {
+                const size_t i = base + u * 256 + threadIdx.x;
+                if (i < n) dst[i] = src[i];
+            }
+        }
+    }
 }
 
 int stream_probe(size_t bytes, int iters, double* gbs) {
@@ -691,19 +712,28 @@ int stream_probe(size_t bytes, int iters, double* gbs) {
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int rc = -1;
+    double best = 0.0;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
         hipEventCreate(&e1) == hipSuccess && hipMemsetAsync(a, 1, n * 16, st) == hipSuccess) {
-        const dim3 grid(device_cus() * 8), blk(256);
-        hipLaunchKernelGGL(k_stream_probe, grid, blk, 0, st, a, b, n);  // warm
-        (void)hipEventRecord(e0, st);
-        for (int i = 0; i < iters; i++) hipLaunchKernelGGL(k_stream_probe, grid, blk, 0, st, a, b, n);
-        (void)hipEventRecord(e1, st);
-        float ms = 0.0f;
-        if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.0f) {
-            *gbs = 2.0 * (double)(n * 16) * iters / (ms * 1e-3) / 1e9;
-            rc = 0;
-        }
+        typedef void (*probe_fn)(const probe_u32x4*, probe_u32x4*, size_t);
+        const probe_fn fns[4] = {k_stream_probe<4, false>, k_stream_probe<4, true>, k_stream_probe<8, false>,
+                                 k_stream_probe<8, true>};
+        for (int wpc : {4, 8, 16})
+            for (probe_fn f : fns) {
+                const dim3 grid(device_cus() * wpc), blk(256);
+                hipLaunchKernelGGL(f, grid, blk, 0, st, a, b, n);  // warm
+                (void)hipEventRecord(e0, st);
+                for (int i = 0; i < iters; i++) hipLaunchKernelGGL(f, grid, blk, 0, st, a, b, n);
+                (void)hipEventRecord(e1, st);
+                float ms = 0.0f;
+                if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess &&
+                    ms > 0.0f) {
+                    best = std::max(best, 2.0 * (double)(n * 16) * iters / (ms * 1e-3) / 1e9);
+                    rc = 0;
+                }
+            }
     }
+    if (rc == 0) *gbs = best;
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (st) (void)hipStreamDestroy(st);

@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void k_sweep_verdict(const int* __restrict__ e
     for (size_t i = tid; i < n * F; i += nth) disp[i] = invalid;
     if (mins)
         for (size_t i = tid; i < (size_t)F * kMinSlots; i += nth) mins[i] = invalid;
-    if (tid == 0) atomicOr(sticky, 1);
+    if (tid == 0) atomicAdd(sticky, 1);  // counts timed-out batches: the host reports each once
 }
 
 void launch_sweep_verdict(const int* err, int16_t* disp, size_t n, int F, int16_t invalid, int* mins,

@@ -1441,11 +1441,24 @@ namespace {
             return sdr::set_error(SDR_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// The sequential solver's exact division needs every pass's pivots in [1, 2^126): each pass's
+// lambda (lambda * attenuation^k, in launch_fgs's float arithmetic) in [0, kFgsThomasMaxLambda]
+// (an attenuation above 1 or below 0 used to pass with only the first checked)
+bool thomas_lambdas_ok(double lambda, double att, int iters) {
+    float lam = (float)lambda;
+    const float fa = (float)att;
+    for (int it = 0; it < iters; it++, lam = lam * fa)
+        if (!(lam >= 0.0f) || !((double)lam <= sdr::kFgsThomasMaxLambda)) return false;
+    return true;
+}
+constexpr const char* kThomasLambdaMsg =
+    "SDR_FGS_THOMAS needs every pass's lambda * attenuation^k in [0, 2^100] (its pivots stay in [1, 2^126))";
+
 int check_wls_params(const sdr_wls_params& p) {
     if (!(p.lambda >= 0.0) || !(p.sigma_color >= 0.0) || p.num_iter < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
-    if (p.fgs_solver == SDR_FGS_THOMAS && p.lambda > sdr::kFgsThomasMaxLambda)
-        return sdr::set_error(SDR_ERR_ARG, "SDR_FGS_THOMAS takes lambda <= 2^100 (its pivots stay below 2^126)");
+    if (p.fgs_solver == SDR_FGS_THOMAS && !thomas_lambdas_ok(p.lambda, p.lambda_attenuation, p.num_iter))
+        return sdr::set_error(SDR_ERR_ARG, kThomasLambdaMsg);
     if (p.fgs_solver != SDR_FGS_PCR && p.fgs_solver != SDR_FGS_THOMAS)
         return sdr::set_error(SDR_ERR_ARG, "fgs_solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
     if (p.depth_discontinuity_radius < 0 || p.left_offset < 0 || p.right_offset < 0 ||
@@ -1759,8 +1772,8 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
         return sdr::set_error(SDR_ERR_ARG, "bad size/stride");
     if (!(lambda >= 0.0) || !(sigma >= 0.0) || iters < 1)
         return sdr::set_error(SDR_ERR_ARG, "FGS needs lambda >= 0, sigma_color >= 0, num_iter >= 1");
-    if (solver == SDR_FGS_THOMAS && lambda > sdr::kFgsThomasMaxLambda)
-        return sdr::set_error(SDR_ERR_ARG, "SDR_FGS_THOMAS takes lambda <= 2^100 (its pivots stay below 2^126)");
+    if (solver == SDR_FGS_THOMAS && !thomas_lambdas_ok(lambda, att, iters))
+        return sdr::set_error(SDR_ERR_ARG, kThomasLambdaMsg);
     if (solver != SDR_FGS_PCR && solver != SDR_FGS_THOMAS)
         return sdr::set_error(SDR_ERR_ARG, "solver must be SDR_FGS_PCR or SDR_FGS_THOMAS");
     if (solver == SDR_FGS_PCR && (w > sdr::kPcrMaxN || h > sdr::kPcrMaxN))

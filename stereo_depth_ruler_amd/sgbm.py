@@ -45,10 +45,25 @@ def _cstream(device_index: int):
     return ctypes.c_void_p(torch.cuda.current_stream(device_index).cuda_stream)
 
 
+STREAM_PERSISTENT = 1  # SDR_STREAM_PERSISTENT (include/sdr/sdr.h)
+
+
+def stream_is_pooled(stream_id: int) -> bool:
+    """True for torch's default stream and its pooled streams, which live as long as the process;
+    False for a torch.cuda.ExternalStream, which its owner may destroy.  c10's StreamId encodes an
+    external stream as the stream pointer itself (even, non-zero: c10/cuda/CUDAStream.cpp
+    streamIdType) and every stream torch allocates with the low bit set (the default stream is 0)."""
+    return stream_id == 0 or (stream_id & 1) == 1
+
+
 def set_handle_stream(h, device_index: int, stream=None):
-    """Points a matcher handle at `stream` (default: the current stream of the device)."""
+    """Points a matcher handle at `stream` (default: the current stream of the device).  torch's
+    own streams are bound persistent (the handle's retire event is recorded only at a stream
+    switch); an external stream is bound transient, so the caller may destroy it after the call
+    (sdr.h sdr_sgbm_set_stream_ex)."""
     s = stream if stream is not None else torch.cuda.current_stream(device_index)
-    check(lib().sdr_sgbm_set_stream(h, ctypes.c_void_p(s.cuda_stream)))
+    flags = STREAM_PERSISTENT if stream_is_pooled(int(s.stream_id)) else 0
+    check(lib().sdr_sgbm_set_stream_ex(h, ctypes.c_void_p(s.cuda_stream), flags))
 
 
 def _Q(Q) -> ctypes.Array:

@@ -167,3 +167,19 @@ def test_sweep_status_host_only():
     L = _lib.lib()
     assert L.sdr_sgbm_last_status(None) == -1
     assert L.sdr_sgbm_debug_knob(None, 1, 4) == -1
+
+
+def test_stream_binding_flags_host_only():
+    """torch's default (id 0) and pooled streams (odd ids) bind persistent; an external stream (its
+    id is the even, non-zero stream pointer: c10 StreamId) binds transient (sdr.h set_stream_ex).
+    Unknown flag bits are refused before any device call."""
+    import ctypes
+
+    from stereo_depth_ruler_amd.sgbm import STREAM_PERSISTENT, stream_is_pooled
+
+    assert STREAM_PERSISTENT == 1
+    assert stream_is_pooled(0)
+    assert stream_is_pooled(1) and stream_is_pooled(0x23) and stream_is_pooled((5 << 5) | 1)
+    assert not stream_is_pooled(0x7F3A12345600)
+    assert _lib.lib().sdr_sgbm_set_stream_ex(None, None, 0) == -1
+    assert _lib.lib().sdr_sgbm_set_stream_ex(ctypes.c_void_p(8), None, 6) == -1

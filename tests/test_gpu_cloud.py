@@ -66,11 +66,15 @@ def test_voxel_passthrough_and_empty(oracle):
     assert empty.points.shape == (0, 4)
 
 
-def test_pcd_write_pipeline(oracle, tmp_path):
-    """pcd_write.cpp:86-141 end to end on the device, checked byte for byte against the oracle."""
-    H, W = 240, 400
-    Lg, Rg, _ = S.make_pair(H, W, 80, seed=41)
-    rng = np.random.default_rng(41)
+@pytest.mark.parametrize("H,W,seed", [(240, 400, 41), (720, 1280, 100)])
+def test_pcd_write_pipeline(oracle, tmp_path, H, W, seed):
+    """pcd_write.cpp:86-141 end to end on the device, checked byte for byte against the oracle.
+    720x1280 is the reference's own geometry: frame 100 of the 2560x720 SBS
+    video split into 1280x720 halves, 3WAY d=80 with the LR check (1) and speckle (200/2) active
+    (pcd_write.cpp:102-116) -- four 180-row stripes with their overlap rows, W1 = 1200 matched
+    columns -- reprojectImageTo3D(handleMissing), the organised cloud and VoxelGrid(5 mm)."""
+    Lg, Rg, _ = S.make_pair(H, W, 80, seed=seed)
+    rng = np.random.default_rng(seed)
     left = np.stack([Lg, np.roll(Lg, 1, 1), rng.integers(0, 256, Lg.shape)], -1).astype(np.uint8)
     right = np.stack([Rg, np.roll(Rg, 1, 1), rng.integers(0, 256, Rg.shape)], -1).astype(np.uint8)
     dev = torch.device("cuda", 0)
@@ -87,8 +91,14 @@ def test_pcd_write_pipeline(oracle, tmp_path):
     # oracle chain
     og_l, og_r = oracle.bgr2gray(left), oracle.bgr2gray(right)
     d = oracle.sgbm_compute(og_l, og_r, oracle.make_params(*args))
-    assert np.array_equal(disp[0].cpu().numpy(), d)
+    got = disp[0].cpu().numpy()
+    assert np.array_equal(got, d), f"{(got != d).sum()} px differ"
+    # the LR check and the speckle filter are both active: each changes the map
+    for off in ((0, 80, 5, 600, 2400, 1000000, 63, 12, 200, 2, sdr.MODE_SGBM_3WAY),
+                (0, 80, 5, 600, 2400, 1, 63, 12, 0, 2, sdr.MODE_SGBM_3WAY)):
+        assert not np.array_equal(oracle.sgbm_compute(og_l, og_r, oracle.make_params(*off)), d)
     oxyz = oracle.reproject(oracle.disp_to_float(d), S.REFERENCE_Q, True)
+    assert np.array_equal(u32(xyz[0].cpu().numpy()), u32(oxyz))
     opts = oracle.xyz_to_cloud(oxyz, left)
     ref, passthrough = oracle.voxel_grid(opts, 0.005)
     assert vg.passthrough == passthrough

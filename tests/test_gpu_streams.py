@@ -94,3 +94,74 @@ def test_caller_stream_destroyed_after_switching_away(oracle):
         for _ in range(2):
             assert np.array_equal(m.compute(L, R)[0].cpu().numpy(), ref)
     m.close()
+
+
+def test_switch_off_a_destroyed_stream(oracle):
+    """VERDICT r5 item 4 (the crash in gpurun_out/r5b/tests.log): a caller's external stream is
+    destroyed right after a call on it, WITHOUT moving the handle off it first; the next call
+    (on another stream), last_status and close() must not touch the dead stream.  An external
+    stream is bound transient (sgbm.set_handle_stream: sdr_sgbm_set_stream_ex without
+    SDR_STREAM_PERSISTENT), so the handle relays its retire event through its own stream at the
+    end of each call.  Bit-exact throughout; also through the raw C ABI's set_stream."""
+    import ctypes
+
+    from stereo_depth_ruler_amd._lib import check, lib
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    H, W, D = 120, 320, 64
+    Ls, Rs = S.make_batch(1, H, W, D, seed0=78)
+    dev = torch.device("cuda", 0)
+    L, R = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    args = (0, D, 5, 600, 2400, 1, 63, 12, 0, 2, sdr.MODE_SGBM)
+    ref = oracle.sgbm_compute(Ls[0], Rs[0], oracle.make_params(*args))
+    for how in ("torch_external", "c_abi", "close_on_dead_stream"):
+        m = sdr.StereoSGBM.create(*args)
+        raw = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+        out = torch.empty((1, H, W), dtype=torch.int16, device=dev)
+        if how == "torch_external":
+            with torch.cuda.stream(torch.cuda.ExternalStream(raw.value, device=dev)):
+                m.compute(L, R, disp=out)
+        else:
+            check(lib().sdr_sgbm_set_stream(m._h, raw))
+            check(lib().sdr_sgbm_compute_device(m._h, ctypes.c_void_p(L.data_ptr()), ctypes.c_void_p(R.data_ptr()),
+                                                W, H, W, H * W, 1, ctypes.c_void_p(out.data_ptr()), W, H * W))
+        assert hip.hipStreamSynchronize(raw) == 0
+        assert hip.hipStreamDestroy(raw) == 0  # the handle is still bound to it
+        assert np.array_equal(out[0].cpu().numpy(), ref)
+        if how == "close_on_dead_stream":
+            check(lib().sdr_sgbm_last_status(m._h))
+            m.close()
+            continue
+        for _ in range(2):  # compute() moves the handle to torch's current stream
+            assert np.array_equal(m.compute(L, R)[0].cpu().numpy(), ref)
+        m.close()
+
+
+def test_transient_stream_orders_next_stream(oracle):
+    """A transient stream's calls are ordered before the next stream's without a host sync: C2-size
+    frames queued on an external stream, then on torch's stream, back to back; every output equals
+    the one-at-a-time run."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    H, W, D, F = 720, 1280, 128, 2
+    Ls, Rs = S.make_batch(2 * F, H, W, D, seed0=910)
+    dev = torch.device("cuda", 0)
+    L, R = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    args = (0, D, 5, 600, 2400, 1, 63, 12, 200, 2, sdr.MODE_SGBM)
+    m = sdr.StereoSGBM.create(*args)
+    refs = _refs(m, L, R, F, 2)
+    raw = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+    outs = [torch.empty((F, H, W), dtype=torch.int16, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(torch.cuda.ExternalStream(raw.value, device=dev)):
+        m.compute(L[:F], R[:F], disp=outs[0])
+    m.compute(L[F:], R[F:], disp=outs[1])
+    torch.cuda.synchronize()
+    assert hip.hipStreamSynchronize(raw) == 0
+    assert hip.hipStreamDestroy(raw) == 0
+    for k in range(2):
+        assert torch.equal(outs[k], refs[k]), k
+    m.close()

@@ -130,6 +130,51 @@ def test_sweep_timeout_reported_by_next_call(oracle):
     m.close()
 
 
+def test_sweep_timeout_reported_once_unsynchronised(oracle):
+    """a timeout is reported exactly once even when later batches are queued before its
+    status copy lands.  The device word counts timed-out batches and the host remembers the count
+    it reported (no clear of the device word that a copy still in flight could undo): one forced
+    timeout, then four calls queued back to back with no synchronisation, then the status --
+    SDR_ERR_DEVICE exactly once over all of them, and the frames after it bit-exact."""
+    F, H, W, D = 16, 96, 1700, 48
+    args = (0, D, 5, 600, 2400, 1, 63, 10, 0, 2, sdr.MODE_HH)
+    Ls, Rs = _batch("textured", F, H, W, D, 42)
+    dev = torch.device("cuda", 0)
+    Ld, Rd = torch.from_numpy(Ls).to(dev), torch.from_numpy(Rs).to(dev)
+    m = sdr.StereoSGBM.create(*args)
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 1)
+    bad = torch.empty((F, H, W), dtype=torch.int16, device=dev)
+    m.compute(Ld, Rd, disp=bad)  # queued, not synchronised
+    m.set_debug_knob(sdr.sgbm.DEBUG_SWEEP_SPIN, 0)
+    errors = 0
+    outs = []
+    for _ in range(4):
+        o = torch.empty((F, H, W), dtype=torch.int16, device=dev)
+        try:
+            m.compute(Ld, Rd, disp=o)
+            outs.append(o)
+        except sdr.SDRError as e:
+            assert e.code == -6
+            errors += 1
+    try:
+        m.check_status()
+    except sdr.SDRError as e:
+        assert e.code == -6
+        errors += 1
+    assert errors == 1, errors
+    assert (bad.cpu().numpy() == -16).all()
+    m.check_status()
+    good = m.compute(Ld, Rd).cpu().numpy()
+    m.check_status()
+    p = oracle.make_params(*args)
+    ref = oracle.sgbm_compute(Ls[F - 1], Rs[F - 1], p)
+    assert np.array_equal(good[F - 1], ref)
+    # calls queued after the timed-out batch in the same stream ran with the default budget
+    for o in outs[1:]:
+        assert np.array_equal(o[F - 1].cpu().numpy(), ref)
+    m.close()
+
+
 def test_two_handles_two_streams_concurrent_sweeps(oracle):
     """Two matchers on two streams each enqueue 8-frame MODE_HH batches back to back without a
     synchronisation in between: their sweeps are chained per device (never two in flight), and

@@ -176,3 +176,36 @@ def test_right_matcher_range(oracle):
     valid = d != -80 * 16
     assert valid.mean() > 0.3
     assert d[valid].min() >= -79 * 16 and d[valid].max() <= 0
+
+
+def test_native_build_matches_portable(oracle, tmp_path):
+    """bench.py's cpu_baseline times the oracle built -O3 -march=native; with FP
+    contraction off it must compute exactly what the portable checker build computes: SGBM (5-path
+    and 3WAY with LR + speckle), the WLS filter and the reprojection, compared bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+from stereo_depth_ruler_amd import synthetic as S
+O.select_build(sys.argv[3])
+L, R, _ = S.make_pair(72, 200, 48, seed=5)
+d5 = O.sgbm_compute(L, R, O.make_params(0, 48, 5, 600, 2400, 1, 63, 12, 100, 2, 0))
+d3 = O.sgbm_compute(L, R, O.make_params(0, 48, 5, 600, 2400, 1, 63, 12, 100, 2, 2))
+dr = O.sgbm_compute(R, L, O.make_params(-47, 48, 5, 600, 2400, 1000000, 63, 0, 0, 2, 2))
+q = O.wls_params_for_sgbm(0, 48, 5, 200, 72, 8000.0, 1.1)
+w = O.wls_filter(d3, dr, L, q)
+x = O.reproject(O.disp_to_float(w), S.REFERENCE_Q, True)
+np.savez(sys.argv[2], d5=d5, d3=d3, w=w, x=x.view(np.uint32))
+'''
+    outs = {}
+    for kind in ("portable", "native"):
+        f = tmp_path / f"{kind}.npz"
+        subprocess.check_call([sys.executable, "-c", script, root, str(f), kind], cwd=root)
+        outs[kind] = np.load(f)
+    for k in ("d5", "d3", "w", "x"):
+        assert np.array_equal(outs["portable"][k], outs["native"][k]), k

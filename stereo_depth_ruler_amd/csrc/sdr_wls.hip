@@ -795,6 +795,308 @@ __global__ __launch_bounds__(256) void k_fgs_th(FgsThArgs a) {
     }
 }
 
+// ---- k_fgs_lr: the sequential pass with its lines resident in LDS (round 6) ----------------
+// The same recurrences, operations and roundings as k_fgs_th (ximgproc's order, bit-exact), for
+// both right-hand sides at once, rebuilt around what bounds a one-wave chain: every instruction
+// the chain's wave issues is on the critical path (a dependent f32 op takes ~4.9 cycles, the
+// issue of the next about 4: nothing hides behind the chain), so the pass time is the solver
+// wave's instruction count per sample times the line length (scripts/probe/fgs_rows.hip).
+//  * one solver wave PER IMAGE (waves 0 and 1, on two SIMDs): scalar chains, 5 dependent ops a
+//    forward sample and 2 a back sample (the packed form issues at 8 cycles an op: no gain);
+//  * lane = (row, line): L <= 16 lines on the 16 lanes of each 16-lane row, and the four rows hold
+//    four consecutive samples each of a 16-sample group, so ONE LDS instruction reads or writes
+//    4 samples x L lines; the chain value walks the rows 0 -> 1 -> 3 -> 2 (one v_permlane16/32_swap
+//    per row change, every 4 samples), every row computing every step (the issue cost is the
+//    wave's whatever the rows), each row keeping its own steps' results (selected per lane at the
+//    group's end: no exec masks);
+//  * the whole line stays in LDS: the loader waves (2 and 3) DMA the pass's input U and its
+//    coefficients (a, den, 1/den, t) once, a chunk of 1024 line-samples at a time, up to
+//    kLrAhead chunks ahead; the forward values overwrite U in place and the back substitution
+//    reads them from there (no global round trip between the two phases, no buffer reuse), its
+//    results overwrite them again and the same two waves store them to global memory a chunk
+//    behind the solvers;
+//  * the reciprocal-form division with the tiny-quotient key per 16-sample group; a group whose
+//    key trips runs again from its start with IEEE divisions (its operands are still in
+//    registers), and a group starting from an already small value (|p| < 2^-64) divides from the
+//    start (the same rule as k_fgs_th's chunks, per 16 samples instead of per chunk).
+// LDS: [U: kLrChunks x 8 KiB][coef: kLrChunks x 16 KiB], sample k of line l at (k * L + l): a line
+// of up to kLrChunks * 1024 / L samples (L = 16: 384, 8: 768, 4: 1536, 2: 3072).  Longer lines
+// take k_fgs_th.
+constexpr int kLrChunks = 6;
+constexpr int kLrU = kLrChunks * 8192, kLrLds = kLrChunks * 24576;
+constexpr int kLrAhead = 4;  // chunks in flight (th_wait_chunks waits for at most 2 beyond)
+static_assert(kLrAhead - 2 <= kThNB - 3, "th_wait_chunks' range");
+
+// the chain value from one lane row to the next in the walk 0 -> 1 -> 3 -> 2 -> 0: the swap of p
+// with itself keeps the source row's value where it was AND copies it into the next row, so the
+// result is both the step's kept value (for the source row) and the next row's chain input
+__device__ __forceinline__ float lr_row(int step, float p) {
+    const int b = __builtin_bit_cast(int, p);
+    if (step == 0) return __builtin_bit_cast(float, (int)__builtin_amdgcn_permlane16_swap(b, b, false, false)[0]);
+    if (step == 1) return __builtin_bit_cast(float, (int)__builtin_amdgcn_permlane32_swap(b, b, false, false)[0]);
+    if (step == 2) return __builtin_bit_cast(float, (int)__builtin_amdgcn_permlane16_swap(b, b, false, false)[1]);
+    return __builtin_bit_cast(float, (int)__builtin_amdgcn_permlane32_swap(b, b, false, false)[1]);
+}
+
+// a lane's own row's value among the walk's four steps (rows 0, 1, 3, 2 take steps 0, 1, 2, 3)
+template <typename T>
+__device__ __forceinline__ T lr_own(const T (&v)[4], bool s0, bool s1, bool s2) {
+    return s0 ? v[0] : s1 ? v[1] : s2 ? v[2] : v[3];
+}
+
+struct LrFwdOps {
+    float4 q[4];  // (a, den, 1/den, t) of the lane's 4 samples
+    float x[4];   // the right-hand side
+};
+struct LrBackOps {
+    float t[4];
+    float x[4];  // the forward values
+};
+
+template <int L>
+struct LrLane {
+    int l, step;     // line within the workgroup, the walk step of the lane's row
+    bool s0, s1, s2;  // step == 0, 1, 2
+    bool valid;       // a real line (l < L and inside the pass)
+    int img4;         // 4 * image (the float2 half)
+};
+
+// forward group g: samples k0 .. k0 + 15 (k0 = 16 g); lane row of step s holds k0 + 4 s + e
+template <int L, bool EXACT, bool GUARD>
+__device__ __forceinline__ void lr_fwd_body(float& p, const LrFwdOps& o, int k0, int n, float (&res)[4][4]) {
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            if (!GUARD || k0 + 4 * s + e < n) {
+                const float x = o.x[e] - o.q[e].x * p;
+                if constexpr (EXACT) {
+                    p = x / o.q[e].y;
+                } else {
+                    const float q0 = x * o.q[e].z;
+                    p = __builtin_fmaf(-__builtin_fmaf(q0, o.q[e].y, -x), o.q[e].z, q0);
+                }
+            }
+            if (e < 3) res[s][e] = p;
+        }
+        p = lr_row(s, p);
+        res[s][3] = p;
+    }
+}
+
+// The group, then its outputs checked: the reciprocal form is exact while |q0| >= 2^-96 (den >= 1,
+// scripts/markstein_check.c); a quotient q0 below that leaves |p| < 2^-95, so any output of the
+// lane's own samples under 2^-95 -- exact zeros included -- runs the group again from its start
+// with IEEE divisions (3 instructions a group on the lane's selected outputs, instead of a key per
+// sample in every row).  A group starting from an already small value (|p| < 2^-64: a decaying run
+// of zero right-hand sides) divides from the start.
+template <int L, bool GUARD>
+__device__ __forceinline__ void lr_fwd_group(float& p, const LrFwdOps& o, const LrLane<L>& ln, int k0, int n,
+                                             char* uw) {
+    float res[4][4];
+    const float ps = p;  // (valid in row 0, where the walk starts)
+    const bool small = __builtin_amdgcn_ballot_w64(ln.valid & ln.s0 & (fabsf(p) < 0x1p-64f)) != 0;
+    if (small) lr_fwd_body<L, true, GUARD>(p, o, k0, n, res);
+    else lr_fwd_body<L, false, GUARD>(p, o, k0, n, res);
+    float out[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const float v[4] = {res[0][e], res[1][e], res[2][e], res[3][e]};
+        out[e] = lr_own(v, ln.s0, ln.s1, ln.s2);
+    }
+    if (!small) {
+        // (samples past the line's end hold copies of the last output: checked like it)
+        const float m = fminf(fminf(fabsf(out[0]), fabsf(out[1])), fminf(fabsf(out[2]), fabsf(out[3])));
+        if (__builtin_amdgcn_ballot_w64(ln.valid & (m < 0x1p-95f))) {
+            p = ps;
+            lr_fwd_body<L, true, GUARD>(p, o, k0, n, res);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float v[4] = {res[0][e], res[1][e], res[2][e], res[3][e]};
+                out[e] = lr_own(v, ln.s0, ln.s1, ln.s2);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++) *(float*)(uw + e * L * 8) = out[e];
+}
+
+// back group gb: samples k1 .. k1 - 15 (k1 = n - 1 - 16 gb); lane row of step s holds k1 - 4 s - e;
+// the last sample keeps its forward value
+template <int L, bool GUARD>
+__device__ __forceinline__ void lr_back_group(float& p, const LrBackOps& o, const LrLane<L>& ln, int k1, int n,
+                                              char* uw) {
+    float res[4][4];
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int k = k1 - 4 * s - e;
+            if (!GUARD || k >= 0) {
+                if (GUARD && k == n - 1) p = o.x[e];
+                else p = o.x[e] - o.t[e] * p;
+            }
+            if (e < 3) res[s][e] = p;
+        }
+        p = lr_row(s, p);
+        res[s][3] = p;
+    }
+    // the lane's samples k1 - 4 s - e sit at uw - e * L * 8 (uw: its first, the highest)
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        const float v[4] = {res[0][e], res[1][e], res[2][e], res[3][e]};
+        if (!GUARD || k1 - 4 * ln.step - e >= 0) *(float*)(uw - e * L * 8) = lr_own(v, ln.s0, ln.s1, ln.s2);
+    }
+}
+
+// The solver wave of image `img` (0: A / U.x, 1: B / U.y).
+template <int L>
+__device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, bool lv, char* lds) {
+    constexpr int CH = 1024 / L;  // samples a chunk
+    constexpr int G = CH / 16;    // groups a chunk
+    LrLane<L> ln;
+    ln.l = lane & 15;
+    const int row = lane >> 4;
+    ln.step = row == 0 ? 0 : row == 1 ? 1 : row == 3 ? 2 : 3;
+    ln.s0 = ln.step == 0;
+    ln.s1 = ln.step == 1;
+    ln.s2 = ln.step == 2;
+    ln.valid = lv && ln.l < L;
+    const int l = ln.l < L ? ln.l : L - 1;  // (lanes past L read line L - 1 and store nothing useful)
+    ln.img4 = img * 4;
+    char* U = lds + img * 4;
+    const char* Cq = lds + kLrU;
+    auto uaddr = [&](int k) __attribute__((always_inline)) { return U + (k * L + l) * 8; };
+    auto ld_fwd = [&](int g, LrFwdOps& o) __attribute__((always_inline)) {
+        const int k = 16 * g + 4 * ln.step;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            o.q[e] = *(const float4*)(Cq + ((k + e) * L + l) * 16);
+            o.x[e] = *(const float*)uaddr(k + e);
+        }
+    };
+    const int ng = (n + 15) / 16;
+    auto fwd = [&](int g, float& p, const LrFwdOps& o) __attribute__((always_inline)) {
+        char* uw = uaddr(16 * g + 4 * ln.step);
+        if (16 * g + 15 < n) lr_fwd_group<L, false>(p, o, ln, 16 * g, n, uw);
+        else lr_fwd_group<L, true>(p, o, ln, 16 * g, n, uw);
+    };
+    // ---- forward elimination: barrier c = chunks <= c + 1 landed ----
+    float p = 0.0f;
+    LrFwdOps A, B;
+    th_barrier();
+    ld_fwd(0, A);
+    for (int c = 0; c < nch; c++) {
+        if (c > 0) th_barrier();
+        for (int gg = 0; gg < G; gg += 2) {
+            const int g = c * G + gg;
+            if (g >= ng) break;
+            if (g + 1 < ng) ld_fwd(g + 1, B);
+            fwd(g, p, A);
+            if (g + 1 >= ng) break;
+            if (g + 2 < ng) ld_fwd(g + 2, A);
+            fwd(g + 1, p, B);
+        }
+    }
+    // the walk's value (p[n-1]) is in row 0; the back substitution reads it back from LDS
+    // ---- back substitution: barrier cb = chunk cb's results in LDS for the writers ----
+    auto ld_back = [&](int gb, LrBackOps& o) __attribute__((always_inline)) {
+        const int k = n - 1 - 16 * gb - 4 * ln.step;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int kk = max(k - e, 0);
+            o.t[e] = *(const float*)(Cq + (kk * L + l) * 16 + 12);
+            o.x[e] = *(const float*)uaddr(kk);
+        }
+    };
+    auto back = [&](int gb, float& q, const LrBackOps& o) __attribute__((always_inline)) {
+        const int k1 = n - 1 - 16 * gb;
+        char* uw = uaddr(max(k1 - 4 * ln.step, 0));
+        if (gb > 0 && k1 - 15 >= 0) lr_back_group<L, false>(q, o, ln, k1, n, uw);
+        else lr_back_group<L, true>(q, o, ln, k1, n, uw);
+    };
+    th_lgkm0();  // (the forward values are read back by this wave only: its own writes, in order)
+    float q = 0.0f;
+    LrBackOps Ab, Bb;
+    ld_back(0, Ab);
+    for (int cb = 0; cb < nch; cb++) {
+        for (int gg = 0; gg < G; gg += 2) {
+            const int gb = cb * G + gg;
+            if (gb >= ng) break;
+            if (gb + 1 < ng) ld_back(gb + 1, Bb);
+            back(gb, q, Ab);
+            if (gb + 1 >= ng) break;
+            if (gb + 2 < ng) ld_back(gb + 2, Ab);
+            back(gb + 1, q, Bb);
+        }
+        th_lgkm0();
+        th_barrier();
+    }
+}
+
+// The loader waves (lw = 0, 1): the pass's U (float2) and coefficient chunks, up to kLrAhead in
+// flight; before barrier c, chunks <= c + 1 have landed.  Then, as writers, the results of back
+// chunk cb after barrier cb: line-major float2 into a.O (the next pass's input), or k-major split
+// into a.O0 / a.O1 (the last pass).
+template <int L>
+__device__ __forceinline__ void lr_loader_writer(const FgsThArgs& a, size_t fofs, int l0, int nch, int lw, int lane,
+                                                 char* lds) {
+    constexpr int CH = 1024 / L, IW = (8 + 16) / 2;
+    const int n = a.n, last = n - 1;
+    const char* gu = (const char*)((const float2*)a.U + fofs);
+    const char* gc = (const char*)(a.coef + fofs);
+    auto issue = [&](int c) __attribute__((always_inline)) {
+        th_issue<L, 8>(gu, a.st, l0, c * CH, 1, last, lds + c * 8192, lw, lane);
+        th_issue<L, 16>(gc, a.st, l0, c * CH, 1, last, lds + kLrU + c * 16384, lw, lane);
+    };
+    int issued = 0;
+    for (; issued < min(kLrAhead, nch); issued++) issue(issued);
+    for (int c = 0; c < nch; c++) {
+        th_wait_chunks<IW>(issued - min(c + 2, issued));
+        th_barrier();
+        if (issued < nch) issue(issued++);
+    }
+    // ---- writers ----
+    const float2* R = (const float2*)lds;
+    for (int cb = 0; cb < nch; cb++) {
+        th_barrier();
+        const int khi = n - cb * CH, klo = max(khi - CH, 0);  // samples [klo, khi)
+        if (a.O) {
+            // line-major: a wave-instruction = 64 consecutive samples of one line
+            for (int l = lw; l < L; l += 2) {
+                if (l0 + l >= a.nl) break;
+                float2* o = (float2*)a.O + fofs + (size_t)(l0 + l) * a.onp;
+                for (int k = klo + lane; k < khi; k += 64) o[k] = R[k * L + l];
+            }
+        } else {
+            // k-major split: a wave-instruction = 64 / L samples x L lines
+            const size_t fo = (size_t)blockIdx.y * a.ofs + l0;
+            const int l = lane % L;
+            for (int k = klo + lw * (64 / L) + lane / L; k < khi; k += 2 * (64 / L)) {
+                if (l0 + l < a.nl) {
+                    const float2 v = R[k * L + l];
+                    a.O0[fo + (size_t)k * a.ost + l] = v.x;
+                    a.O1[fo + (size_t)k * a.ost + l] = v.y;
+                }
+            }
+        }
+    }
+}
+
+// One FGS pass of two right-hand sides (a.U float2), L lines a workgroup, every line resident.
+template <int L>
+__global__ __launch_bounds__(256) void k_fgs_lr(FgsThArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[kLrLds];
+    constexpr int CH = 1024 / L;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const size_t fofs = (size_t)blockIdx.y * a.fs;
+    const int l0 = blockIdx.x * L;
+    const int nch = (a.n + CH - 1) / CH;
+    if (wave < 2) lr_solver<L>(a.n, nch, wave, lane, l0 + (lane & 15) < a.nl, lds);
+    else lr_loader_writer<L>(a, fofs, l0, nch, wave - 2, lane, lds);
+}
+
 // R0 (and R1) row-major [h][w] -> the first row pass's input: transposed [w][hp] (hp = h rounded
 // up to 4, frames fgs_pad4(w) * hp apart), the two images interleaved (float2) when R1 is given;
 // 64x64 LDS tiles
@@ -1265,6 +1567,23 @@ static void launch_fgs_th(FgsThArgs a, bool pass, bool two, int F, hipStream_t s
     else launch_fgs_th_lpb<64>(grid, a, two, st);
 }
 
+// One k_fgs_lr launch when the pass's lines fit in LDS (two right-hand sides, n <= 6 * 1024 / L
+// for some L of 16, 8, 4, 2 lines a workgroup: the largest that fits); false: take k_fgs_th.
+static bool launch_fgs_lr(const FgsThArgs& a, bool two, int F, hipStream_t st) {
+    static const bool off = getenv("SDR_FGS_LR") && atoi(getenv("SDR_FGS_LR")) == 0;  // A/B knob
+    if (!two || off) return false;
+    for (int L : {16, 8, 4, 2}) {
+        if (a.n > kLrChunks * 1024 / L) continue;
+        const dim3 grid((a.nl + L - 1) / L, F);
+        if (L == 16) hipLaunchKernelGGL(k_fgs_lr<16>, grid, dim3(256), 0, st, a);
+        else if (L == 8) hipLaunchKernelGGL(k_fgs_lr<8>, grid, dim3(256), 0, st, a);
+        else if (L == 4) hipLaunchKernelGGL(k_fgs_lr<4>, grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_fgs_lr<2>, grid, dim3(256), 0, st, a);
+        return true;
+    }
+    return false;
+}
+
 // k_fgs_pcr instance for G*n samples per block: one equation per thread up to 1024 samples
 // (T = the samples rounded up to whole waves), 2 or 4 per thread of 1024 beyond
 template <bool TWO, bool FIN = false>
@@ -1385,7 +1704,8 @@ static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, con
         }
         for (int p = 0; p < npass; p++) {
             KScope kt(timer, SDR_KERNEL_FGS);
-            launch_fgs_th(pass_args(p), true, two, F, st);
+            const FgsThArgs a = pass_args(p);
+            if (!launch_fgs_lr(a, two, F, st)) launch_fgs_th(a, true, two, F, st);
         }
         return 0;
     }

@@ -636,14 +636,15 @@ def main():
         return kern, roof
 
     def fgs_model(per_kind, corr, all_corr, steps):
-        """The class path's sequential FGS passes (k_fgs_th, SDR_FGS_THOMAS: ximgproc's order) as a
-        latency-bound kernel.  A pass solves every line of the WLS ROI (rows: rh lines of rw
-        samples, columns: rw lines of rh) with one lane per line: each line is a chain of rw (or rh)
-        forward steps then as many back steps, each step a dependent sequence of packed-f32 ops --
-        5 forward (the right-hand sides' elimination from the precomputed coefficients: mul, the
-        Markstein correction fma, fma, and the two-image pack), 2 back (fma, mul) -- at 8.4 cycles
-        a dependent op on one wave (profiles/r5_probe_fgs_step.txt).  floor = the chain's
-        dependent-op cycles at the peak clock; frac = floor / measured pass time."""
+        """The class path's sequential FGS passes (SDR_FGS_THOMAS: ximgproc's order) as a
+        latency-bound kernel: k_fgs_lr (round 6, lines resident in LDS, one solver wave per
+        right-hand side) or k_fgs_th.  A pass solves every line of the WLS ROI (rows: rh lines of
+        rw samples, columns: rw lines of rh): each line is a chain of rw (or rh) forward steps then
+        as many back steps, each step a dependent sequence of f32 ops -- 5 forward (a*p, x - a*p,
+        q0 = x/den by the reciprocal, the Markstein remainder fma, the correction fma), 2 back
+        (t*q, x - t*q) -- at 4.9 cycles a dependent op on one wave (profiles/r5_probe_fgs_step.txt,
+        v_fma_f32 chain).  floor = the chain's dependent-op cycles at the peak clock; frac = floor /
+        measured pass time."""
         tot, cnt = per_kind["fgs_pass"]
         if not cnt:
             return None
@@ -651,15 +652,16 @@ def main():
         rw, rh = roi[2], roi[3]
         # the passes alternate rows and columns (3 iterations: 3 + 3 per frame)
         chain = (rw + rh) / 2.0
-        cyc_op, fwd_ops, back_ops = 8.4, 5, 2
+        cyc_op, fwd_ops, back_ops = 4.9, 5, 2
         floor_us = chain * (fwd_ops + back_ops) * cyc_op / (CLOCK_GHZ * 1e3)
         avg_us = tot / cnt * 1e3
         samples = nmatch // 2 * batch * rw * rh  # line-samples one pass solves (both images together)
         coef = per_kind["fgs_coef"]
         return {
             "bound": "latency",
-            "kernel": "k_fgs_th (sequential FGS pass, SDR_FGS_THOMAS: one lane per line, the solver wave "
-                      "reads only LDS, DMA loader waves and a writer wave beside it)",
+            "kernel": "k_fgs_lr (sequential FGS pass, SDR_FGS_THOMAS: the lines resident in LDS, one solver "
+                      "wave per right-hand side, 4 samples x up to 16 lines a lane-instruction, two DMA "
+                      "loader / writer waves beside them)",
             "achieved": round(samples / (avg_us * 1e-6) / 1e9, 3),
             "peak": round(samples / (floor_us * 1e-6) / 1e9, 3),
             "unit": "G line-samples/s",

@@ -8,17 +8,21 @@
 //   k_xyz_to_cloud   thread per pixel: 12 B XYZ + 3 B BGR in, 16 B out (HBM-bound, streaming)
 //   voxel grid       k_minmax (two-stage, exact float min/max over finite points) -> host decides
 //                    PCL's int32-overflow passthrough -> k_voxel_keys (64-bit key = voxel index <<
-//                    32 | point index, non-finite last) -> hipcub radix sort -> k_voxel_heads +
-//                    hipcub exclusive scan -> k_voxel_centroid (one thread per voxel sums its run in
-//                    point order: the oracle's order, so centroids match bit for bit)
+//                    32 | point index, non-finite last) -> the sort of those keys: a stable LSD
+//                    radix sort of the voxel indices (8-bit digits, as many passes as the largest
+//                    index needs; points start in index order, so stability gives PCL's (index,
+//                    point) order) -> k_voxel_heads + an exclusive scan -> k_voxel_centroid (one
+//                    thread per voxel sums its run in point order: the oracle's order, so
+//                    centroids match bit for bit).  Sort and scan are hand-written (k_rs_*, k_scan_*):
+//                    no library on the path.
 #include "../../include/sdr/sdr.h"
 #include "sdr_internal.hpp"
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -150,6 +154,155 @@ __global__ __launch_bounds__(256) void k_voxel_centroid(const float4* __restrict
     out[pos[i]] = o;
 }
 
+// ---- exclusive scan of int32 (reduce, scan the block totals, apply) ----------------------------
+constexpr int kScanItems = 8, kScanSeg = 256 * kScanItems;
+
+// the block's exclusive prefix of one int per thread (256 threads), and the block total
+__device__ __forceinline__ int block_excl_scan(int v, int* total, int* lds /* [4] */) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int c = lds[i];
+        before += i < w ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const int* __restrict__ in, int n, int* __restrict__ partial) {
+    __shared__ int lds[4];
+    const int base = blockIdx.x * kScanSeg + threadIdx.x * kScanItems;
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) s += base + i < n ? in[base + i] : 0;
+    int tot;
+    (void)block_excl_scan(s, &tot, lds);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of the nb block totals in place, 256 at a time with a carry
+__global__ __launch_bounds__(256) void k_scan_partials(int* __restrict__ partial, int nb) {
+    __shared__ int lds[4];
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 256) {
+        const int i = b0 + threadIdx.x;
+        const int v = i < nb ? partial[i] : 0;
+        int tot;
+        const int ex = block_excl_scan(v, &tot, lds);
+        if (i < nb) partial[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(const int* __restrict__ in, int n, const int* __restrict__ partial,
+                                                    int* __restrict__ out) {
+    __shared__ int lds[4];
+    const int base = blockIdx.x * kScanSeg + threadIdx.x * kScanItems;
+    int v[kScanItems], s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        v[i] = base + i < n ? in[base + i] : 0;
+        s += v[i];
+    }
+    int tot;
+    int run = partial[blockIdx.x] + block_excl_scan(s, &tot, lds);
+#pragma unroll
+    for (int i = 0; i < kScanItems; i++) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+}
+
+// ---- stable LSD radix sort of (32-bit key, 32-bit value) pairs, 8-bit digits ------------------
+constexpr int kRsRounds = 16, kRsTile = 256 * kRsRounds;
+
+// hist[d * nb + b] = keys of tile b with digit d (digit-major: the scan of this array in order is
+// every key's bucket start for the stable scatter)
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ keys, int n, int shift,
+                                                 int* __restrict__ hist, int nb) {
+    __shared__ int h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const int base = blockIdx.x * kRsTile;
+    for (int r = 0; r < kRsRounds; r++) {
+        const int i = base + r * 256 + threadIdx.x;
+        if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1);
+    }
+    __syncthreads();
+    hist[threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+// tile b's keys to their scanned bucket positions in input order: per round of 256 keys, a key's
+// rank among the wave's equal digits (8 ballots), the waves before it (their per-digit counts in
+// LDS) and the rounds before it (the running bucket starts)
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                    int n, int shift, const int* __restrict__ hist, int nb,
+                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out) {
+    __shared__ int start[256];
+    __shared__ int wcnt[4][256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    start[t] = hist[t * nb + blockIdx.x];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int base = blockIdx.x * kRsTile;
+    for (int r = 0; r < kRsRounds; r++) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) wcnt[q][t] = 0;
+        __syncthreads();
+        const int i = base + r * 256 + t;
+        const bool valid = i < n;
+        const uint32_t k = valid ? keys[i] : 0u;
+        const uint32_t v = valid ? vals[i] : 0u;
+        const uint32_t d = (k >> shift) & 255u;
+        uint64_t m = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint64_t bb = __builtin_amdgcn_ballot_w64(valid && ((d >> b) & 1u));
+            m &= (d >> b) & 1u ? bb : ~bb;
+        }
+        const int rank = __popcll(m & lt);
+        if (valid && rank == 0) wcnt[w][d] = __popcll(m);
+        __syncthreads();
+        if (valid) {
+            int off = start[d] + rank;
+            for (int q = 0; q < w; q++) off += wcnt[q][d];
+            keys_out[off] = k;
+            vals_out[off] = v;
+        }
+        __syncthreads();
+        start[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    }
+}
+
+// the voxel index of a point (prod for the non-finite ones, which sort last) and its index
+__global__ __launch_bounds__(256) void k_voxel_split(const uint64_t* __restrict__ keys, int n, uint32_t past,
+                                                     uint32_t* __restrict__ k32, uint32_t* __restrict__ v32) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    k32[i] = k == ~0ull ? past : (uint32_t)(k >> 32);
+    v32[i] = (uint32_t)i;
+}
+
+// back to the 64-bit keys k_voxel_heads / k_voxel_centroid read (voxel << 32 | point, ~0 non-finite)
+__global__ __launch_bounds__(256) void k_voxel_join(const uint32_t* __restrict__ k32, const uint32_t* __restrict__ v32,
+                                                    int n, uint32_t past, uint64_t* __restrict__ keys) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = k32[i];
+    keys[i] = k == past ? ~0ull : ((uint64_t)k << 32) | v32[i];
+}
+
 }  // namespace sdr
 
 namespace {
@@ -257,19 +410,42 @@ int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float
     uint64_t* sorted = (uint64_t*)scratch.get(sizeof(uint64_t) * n);
     int* head = (int*)scratch.get(sizeof(int) * n);
     int* pos = (int*)scratch.get(sizeof(int) * n);
-    if (!keys || !sorted || !head || !pos) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+    // the sort's ping-pong (voxel, point) arrays and its histograms; the scan's block totals
+    uint32_t* kv[4];
+    for (auto& q : kv) q = (uint32_t*)scratch.get(sizeof(uint32_t) * n);
+    const int nb_rs = (n + sdr::kRsTile - 1) / sdr::kRsTile;
+    const int nh = 256 * nb_rs;
+    int* hist = (int*)scratch.get(sizeof(int) * nh);
+    const int nb_scan = (std::max(n, nh) + sdr::kScanSeg - 1) / sdr::kScanSeg;
+    int* spart = (int*)scratch.get(sizeof(int) * nb_scan);
+    if (!keys || !sorted || !head || !pos || !kv[0] || !kv[1] || !kv[2] || !kv[3] || !hist || !spart)
+        return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
     const dim3 grid((n + 255) / 256);
+    auto scan = [&](const int* in, int m, int* o) {
+        const int nb = (m + sdr::kScanSeg - 1) / sdr::kScanSeg;
+        hipLaunchKernelGGL(sdr::k_scan_reduce, dim3(nb), dim3(256), 0, st, in, m, spart);
+        hipLaunchKernelGGL(sdr::k_scan_partials, dim3(1), dim3(256), 0, st, spart, nb);
+        hipLaunchKernelGGL(sdr::k_scan_apply, dim3(nb), dim3(256), 0, st, in, m, spart, o);
+    };
     hipLaunchKernelGGL(sdr::k_voxel_keys, grid, dim3(256), 0, st, p, n, v, keys);
-    size_t tb_sort = 0, tb_scan = 0;
-    CLOUD_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb_sort, keys, sorted, n, 0, 64, st));
-    CLOUD_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb_scan, head, pos, n, st));
-    void* tmp = scratch.get(std::max(tb_sort, tb_scan));
-    if (!tmp) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
-    size_t tb = tb_sort;
-    CLOUD_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tb, keys, sorted, n, 0, 64, st));
+    // voxel indices are below div0 * div1 * div2 (each div at most one above PCL's d, whose product
+    // passed the overflow check); `past` = that bound marks the non-finite points, which sort last
+    const unsigned long long divprod = (unsigned long long)div[0] * (unsigned long long)div[1] * (unsigned long long)div[2];
+    const uint32_t past = divprod < 0xFFFFFFFFull ? (uint32_t)divprod : 0xFFFFFFFFu;
+    int bits = 1;
+    while (bits < 32 && (past >> bits) != 0) bits++;
+    hipLaunchKernelGGL(sdr::k_voxel_split, grid, dim3(256), 0, st, keys, n, past, kv[0], kv[1]);
+    int cur = 0;
+    for (int shift = 0; shift < bits; shift += 8) {
+        hipLaunchKernelGGL(sdr::k_rs_hist, dim3(nb_rs), dim3(256), 0, st, kv[cur], n, shift, hist, nb_rs);
+        scan(hist, nh, hist);
+        hipLaunchKernelGGL(sdr::k_rs_scatter, dim3(nb_rs), dim3(256), 0, st, kv[cur], kv[cur + 1], n, shift, hist,
+                           nb_rs, kv[2 - cur], kv[3 - cur]);
+        cur = 2 - cur;
+    }
+    hipLaunchKernelGGL(sdr::k_voxel_join, grid, dim3(256), 0, st, kv[cur], kv[cur + 1], n, past, sorted);
     hipLaunchKernelGGL(sdr::k_voxel_heads, grid, dim3(256), 0, st, sorted, n, head);
-    tb = tb_scan;
-    CLOUD_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, head, pos, n, st));
+    scan(head, n, pos);
     hipLaunchKernelGGL(sdr::k_voxel_centroid, grid, dim3(256), 0, st, p, sorted, n, head, pos, out);
     CLOUD_HIP(hipGetLastError());
     int last_pos = 0, last_head = 0;

@@ -268,6 +268,7 @@ struct FgsThArgs {
     int onp;                // O's line stride (n rounded up to 4: the next pass's st)
     size_t fs;              // frame stride of U, coef, tt, O
     size_t ost, ofs;
+    int dbg;                // diagnostic builds (SDR_TH_STAMPS): the k_fgs_lr stamp slot
     int main_blocks;        // blocks of the pass itself; blocks past them run coefficient jobs
     int njobs;
     FgsCoefJob job[kFgsMaxJobs];
@@ -950,8 +951,27 @@ __device__ __forceinline__ void lr_back_group(float& p, const LrBackOps& o, cons
 }
 
 // The solver wave of image `img` (0: A / U.x, 1: B / U.y).
+#ifdef SDR_TH_STAMPS
+// diagnostic build only: per workgroup of the first 512 of each of 16 launch slots (scripts/lr_stamps.py):
+// 0 entry, 1 first chunk landed, 2 forward done, 3 back done (solver 0), 4 writer done, 5 solver exit,
+// 6 entry s_memrealtime (100 MHz)
+__device__ unsigned long long g_lr_blk[16][512][8];
+#define LR_STAMP(cond, slot, i)                                                                      \
+    do {                                                                                             \
+        if ((cond) && (slot) >= 0 && (threadIdx.x & 63) == 0 && blockIdx.x < 512 && blockIdx.y == 0) { \
+            g_lr_blk[(slot) & 15][blockIdx.x][i] = __builtin_amdgcn_s_memtime();                     \
+            if ((i) == 0) g_lr_blk[(slot) & 15][blockIdx.x][6] = __builtin_amdgcn_s_memrealtime();    \
+            if ((i) == 5) g_lr_blk[(slot) & 15][blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();    \
+        }                                                                                            \
+    } while (0)
+#else
+#define LR_STAMP(cond, slot, i) \
+    do {                        \
+    } while (0)
+#endif
+
 template <int L>
-__device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, bool lv, char* lds) {
+__device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, bool lv, char* lds, int dbg) {
     constexpr int CH = 1024 / L;  // samples a chunk
     constexpr int G = CH / 16;    // groups a chunk
     LrLane<L> ln;
@@ -985,6 +1005,7 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
     float p = 0.0f;
     LrFwdOps A, B;
     th_barrier();
+    LR_STAMP(img == 0, dbg, 1);
     ld_fwd(0, A);
     for (int c = 0; c < nch; c++) {
         if (c > 0) th_barrier();
@@ -1015,6 +1036,7 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
         if (gb > 0 && k1 - 15 >= 0) lr_back_group<L, false>(q, o, ln, k1, n, uw);
         else lr_back_group<L, true>(q, o, ln, k1, n, uw);
     };
+    LR_STAMP(img == 0, dbg, 2);
     th_lgkm0();  // (the forward values are read back by this wave only: its own writes, in order)
     float q = 0.0f;
     LrBackOps Ab, Bb;
@@ -1032,6 +1054,7 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
         th_lgkm0();
         th_barrier();
     }
+    LR_STAMP(img == 0, dbg, 3);
 }
 
 // The loader waves (lw = 0, 1): the pass's U (float2) and coefficient chunks, up to kLrAhead in
@@ -1093,8 +1116,11 @@ __global__ __launch_bounds__(256) void k_fgs_lr(FgsThArgs a) {
     const size_t fofs = (size_t)blockIdx.y * a.fs;
     const int l0 = blockIdx.x * L;
     const int nch = (a.n + CH - 1) / CH;
-    if (wave < 2) lr_solver<L>(a.n, nch, wave, lane, l0 + (lane & 15) < a.nl, lds);
+    LR_STAMP(wave == 0, a.dbg, 0);
+    if (wave < 2) lr_solver<L>(a.n, nch, wave, lane, l0 + (lane & 15) < a.nl, lds, a.dbg);
     else lr_loader_writer<L>(a, fofs, l0, nch, wave - 2, lane, lds);
+    LR_STAMP(wave == 2, a.dbg, 4);
+    LR_STAMP(wave == 0, a.dbg, 5);
 }
 
 // R0 (and R1) row-major [h][w] -> the first row pass's input: transposed [w][hp] (hp = h rounded
@@ -1569,9 +1595,15 @@ static void launch_fgs_th(FgsThArgs a, bool pass, bool two, int F, hipStream_t s
 
 // One k_fgs_lr launch when the pass's lines fit in LDS (two right-hand sides, n <= 6 * 1024 / L
 // for some L of 16, 8, 4, 2 lines a workgroup: the largest that fits); false: take k_fgs_th.
-static bool launch_fgs_lr(const FgsThArgs& a, bool two, int F, hipStream_t st) {
+static bool launch_fgs_lr(FgsThArgs a, bool two, int F, hipStream_t st) {
     static const bool off = getenv("SDR_FGS_LR") && atoi(getenv("SDR_FGS_LR")) == 0;  // A/B knob
     if (!two || off) return false;
+#ifdef SDR_TH_STAMPS
+    static int slot = 0;
+    a.dbg = slot++ & 15;
+#else
+    a.dbg = -1;
+#endif
     for (int L : {16, 8, 4, 2}) {
         if (a.n > kLrChunks * 1024 / L) continue;
         const dim3 grid((a.nl + L - 1) / L, F);
@@ -2074,6 +2106,9 @@ int sdr_fgs_rcp_selftest(int e, unsigned int* mismatches) {
 // diagnostic build only: the stamps of the launch SDR_TH_STAMP_LAUNCH names ([5][1024] u64)
 int sdr_th_blocks(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_blk), 512 * 3 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int sdr_lr_blocks(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_lr_blk), 16 * 512 * 8 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 int sdr_th_counts(unsigned int* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_counts), 16, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;

@@ -862,11 +862,15 @@ struct LrLane {
     int img4;         // 4 * image (the float2 half)
 };
 
-// forward group g: samples k0 .. k0 + 15 (k0 = 16 g); lane row of step s holds k0 + 4 s + e
-template <int L, bool EXACT, bool GUARD>
-__device__ __forceinline__ void lr_fwd_body(float& p, const LrFwdOps& o, int k0, int n, float (&res)[4][4]) {
+// forward group: samples k0 .. k0 + 15 (k0 = 16 g); lane row of walk step s holds k0 + 4 s + e.
+// The reciprocal form keeps per walk step the tiny-quotient key of its row's steps (kk[s]: each
+// row's own is selected after the group).
+template <bool EXACT, bool GUARD>
+__device__ __forceinline__ void lr_fwd_body(float& p, const LrFwdOps& o, int k0, int n, float (&res)[4][4],
+                                            uint32_t (&kk)[4]) {
 #pragma unroll
     for (int s = 0; s < 4; s++) {
+        if constexpr (!EXACT) kk[s] = 0xffffffffu;
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             if (!GUARD || k0 + 4 * s + e < n) {
@@ -876,54 +880,43 @@ __device__ __forceinline__ void lr_fwd_body(float& p, const LrFwdOps& o, int k0,
                 } else {
                     const float q0 = x * o.q[e].z;
                     p = __builtin_fmaf(-__builtin_fmaf(q0, o.q[e].y, -x), o.q[e].z, q0);
+                    kk[s] = min(kk[s], fgs_tiny_key(q0));
                 }
             }
             if (e < 3) res[s][e] = p;
         }
-        p = lr_row(s, p);
+        p = lr_row(s, p);  // keeps the row's value and hands it to the next row
         res[s][3] = p;
     }
 }
 
-// The group, then its outputs checked: the reciprocal form is exact while |q0| >= 2^-96 (den >= 1,
-// scripts/markstein_check.c); a quotient q0 below that leaves |p| < 2^-95, so any output of the
-// lane's own samples under 2^-95 -- exact zeros included -- runs the group again from its start
-// with IEEE divisions (3 instructions a group on the lane's selected outputs, instead of a key per
-// sample in every row).  A group starting from an already small value (|p| < 2^-64: a decaying run
-// of zero right-hand sides) divides from the start.
+// The group with the reciprocal form, or with IEEE divisions when it starts from an already small
+// value (0 < |p| < 2^-64: a decaying run of zero right-hand sides) or when a quotient came out
+// 0 < |q0| < 2^-96 (outside what the reciprocal form covers, scripts/markstein_check.c): then
+// again from the group's start value.  k_fgs_th's rules, per 16 samples.
 template <int L, bool GUARD>
 __device__ __forceinline__ void lr_fwd_group(float& p, const LrFwdOps& o, const LrLane<L>& ln, int k0, int n,
                                              char* uw) {
     float res[4][4];
+    uint32_t kk[4];
     const float ps = p;  // (valid in row 0, where the walk starts)
-    const bool small = __builtin_amdgcn_ballot_w64(ln.valid & ln.s0 & (fabsf(p) < 0x1p-64f)) != 0;
-    if (small) lr_fwd_body<L, true, GUARD>(p, o, k0, n, res);
-    else lr_fwd_body<L, false, GUARD>(p, o, k0, n, res);
-    float out[4];
+    const uint32_t small = 0x3EFFFFFFu;  // fgs_tiny_key(p) < small <=> 0 < |p| < 2^-64
+    bool exact = __builtin_amdgcn_ballot_w64(ln.valid & ln.s0 & (fgs_tiny_key(p) < small)) != 0;
+    if (!exact) {
+        lr_fwd_body<false, GUARD>(p, o, k0, n, res, kk);
+        exact = __builtin_amdgcn_ballot_w64(ln.valid & (lr_own(kk, ln.s0, ln.s1, ln.s2) < kFgsTinyKey)) != 0;
+        if (exact) p = ps;
+    }
+    if (exact) lr_fwd_body<true, GUARD>(p, o, k0, n, res, kk);
 #pragma unroll
     for (int e = 0; e < 4; e++) {
         const float v[4] = {res[0][e], res[1][e], res[2][e], res[3][e]};
-        out[e] = lr_own(v, ln.s0, ln.s1, ln.s2);
+        if (!GUARD || k0 + 4 * ln.step + e < n) *(float*)(uw + e * L * 8) = lr_own(v, ln.s0, ln.s1, ln.s2);
     }
-    if (!small) {
-        // (samples past the line's end hold copies of the last output: checked like it)
-        const float m = fminf(fminf(fabsf(out[0]), fabsf(out[1])), fminf(fabsf(out[2]), fabsf(out[3])));
-        if (__builtin_amdgcn_ballot_w64(ln.valid & (m < 0x1p-95f))) {
-            p = ps;
-            lr_fwd_body<L, true, GUARD>(p, o, k0, n, res);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const float v[4] = {res[0][e], res[1][e], res[2][e], res[3][e]};
-                out[e] = lr_own(v, ln.s0, ln.s1, ln.s2);
-            }
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; e++) *(float*)(uw + e * L * 8) = out[e];
 }
 
-// back group gb: samples k1 .. k1 - 15 (k1 = n - 1 - 16 gb); lane row of step s holds k1 - 4 s - e;
-// the last sample keeps its forward value
+// back group: samples k1 .. k1 - 15 (k1 = n - 1 - 16 gb); lane row of walk step s holds
+// k1 - 4 s - e; the line's last sample keeps its forward value
 template <int L, bool GUARD>
 __device__ __forceinline__ void lr_back_group(float& p, const LrBackOps& o, const LrLane<L>& ln, int k1, int n,
                                               char* uw) {
@@ -950,7 +943,6 @@ __device__ __forceinline__ void lr_back_group(float& p, const LrBackOps& o, cons
     }
 }
 
-// The solver wave of image `img` (0: A / U.x, 1: B / U.y).
 #ifdef SDR_TH_STAMPS
 // diagnostic build only: per workgroup of the first 512 of each of 16 launch slots (scripts/lr_stamps.py):
 // 0 entry, 1 first chunk landed, 2 forward done, 3 back done (solver 0), 4 writer done, 5 solver exit,
@@ -970,10 +962,17 @@ __device__ unsigned long long g_lr_blk[16][512][8];
     } while (0)
 #endif
 
+// The solver wave of image `img` (0: A / U.x, 1: B / U.y).  The whole groups of a chunk run in
+// unrolled blocks of up to 8 with the next group's operands loaded during the current one into a
+// second, static register set (a loop-carried pair made the compiler copy the loads and wait for
+// each right away); every load is unconditional, clamped inside the chunk images (a conditional
+// load made it wait for all of them).  The partial groups -- the line's last forward group, the
+// back groups holding its last and its first samples -- take the guarded form.
 template <int L>
 __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, bool lv, char* lds, int dbg) {
     constexpr int CH = 1024 / L;  // samples a chunk
     constexpr int G = CH / 16;    // groups a chunk
+    constexpr int UB = G < 8 ? G : 8;  // groups an unrolled block
     LrLane<L> ln;
     ln.l = lane & 15;
     const int row = lane >> 4;
@@ -982,75 +981,93 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
     ln.s1 = ln.step == 1;
     ln.s2 = ln.step == 2;
     ln.valid = lv && ln.l < L;
-    const int l = ln.l < L ? ln.l : L - 1;  // (lanes past L read line L - 1 and store nothing useful)
+    const int l = ln.l < L ? ln.l : L - 1;  // (lanes past L repeat line L - 1: the same values)
     ln.img4 = img * 4;
     char* U = lds + img * 4;
     const char* Cq = lds + kLrU;
+    const int kmax = nch * CH - 1;  // the last sample slot of the chunk images
     auto uaddr = [&](int k) __attribute__((always_inline)) { return U + (k * L + l) * 8; };
     auto ld_fwd = [&](int g, LrFwdOps& o) __attribute__((always_inline)) {
-        const int k = 16 * g + 4 * ln.step;
+        const int k = min(16 * g + 4 * ln.step, kmax - 3);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             o.q[e] = *(const float4*)(Cq + ((k + e) * L + l) * 16);
             o.x[e] = *(const float*)uaddr(k + e);
         }
     };
-    const int ng = (n + 15) / 16;
-    auto fwd = [&](int g, float& p, const LrFwdOps& o) __attribute__((always_inline)) {
-        char* uw = uaddr(16 * g + 4 * ln.step);
-        if (16 * g + 15 < n) lr_fwd_group<L, false>(p, o, ln, 16 * g, n, uw);
-        else lr_fwd_group<L, true>(p, o, ln, 16 * g, n, uw);
-    };
+    const int ng = (n + 15) / 16, ngf = n / 16;  // groups of the line, whole ones
     // ---- forward elimination: barrier c = chunks <= c + 1 landed ----
     float p = 0.0f;
-    LrFwdOps A, B;
     th_barrier();
     LR_STAMP(img == 0, dbg, 1);
-    ld_fwd(0, A);
     for (int c = 0; c < nch; c++) {
         if (c > 0) th_barrier();
-        for (int gg = 0; gg < G; gg += 2) {
-            const int g = c * G + gg;
-            if (g >= ng) break;
-            if (g + 1 < ng) ld_fwd(g + 1, B);
-            fwd(g, p, A);
-            if (g + 1 >= ng) break;
-            if (g + 2 < ng) ld_fwd(g + 2, A);
-            fwd(g + 1, p, B);
+        for (int b0 = c * G; b0 < min(c * G + G, ngf); b0 += UB) {
+            LrFwdOps A, B;
+            ld_fwd(b0, A);
+#pragma unroll
+            for (int gg = 0; gg < UB; gg++) {
+                const int g = b0 + gg;
+                LrFwdOps& cur = gg & 1 ? B : A;
+                LrFwdOps& nxt = gg & 1 ? A : B;
+                if (gg + 1 < UB) ld_fwd(g + 1, nxt);
+                if (g < ngf) lr_fwd_group<L, false>(p, cur, ln, 16 * g, n, uaddr(16 * g + 4 * ln.step));
+            }
+        }
+        if (ngf < ng && ngf >= c * G && ngf < c * G + G) {  // the partial last group is in this chunk
+            LrFwdOps A;
+            const int k = 16 * ngf + 4 * ln.step;  // (each sample clamped on its own: the mapping holds)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                A.q[e] = *(const float4*)(Cq + (min(k + e, kmax) * L + l) * 16);
+                A.x[e] = *(const float*)uaddr(min(k + e, kmax));
+            }
+            lr_fwd_group<L, true>(p, A, ln, 16 * ngf, n, uaddr(min(16 * ngf + 4 * ln.step, kmax)));
         }
     }
-    // the walk's value (p[n-1]) is in row 0; the back substitution reads it back from LDS
+    LR_STAMP(img == 0, dbg, 2);
     // ---- back substitution: barrier cb = chunk cb's results in LDS for the writers ----
+    // back group gb: samples k1 .. k1 - 15, k1 = n - 1 - 16 gb: gb = 0 holds the last sample,
+    // gb = ngf the first ones when n % 16 != 0 (guarded); the others are whole
     auto ld_back = [&](int gb, LrBackOps& o) __attribute__((always_inline)) {
-        const int k = n - 1 - 16 * gb - 4 * ln.step;
+        const int k = max(n - 1 - 16 * gb - 4 * ln.step, 3);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            const int kk = max(k - e, 0);
-            o.t[e] = *(const float*)(Cq + (kk * L + l) * 16 + 12);
-            o.x[e] = *(const float*)uaddr(kk);
+            o.t[e] = *(const float*)(Cq + ((k - e) * L + l) * 16 + 12);
+            o.x[e] = *(const float*)uaddr(k - e);
         }
     };
-    auto back = [&](int gb, float& q, const LrBackOps& o) __attribute__((always_inline)) {
+    auto back_guarded = [&](int gb, float& q) __attribute__((always_inline)) {
+        LrBackOps A;
         const int k1 = n - 1 - 16 * gb;
-        char* uw = uaddr(max(k1 - 4 * ln.step, 0));
-        if (gb > 0 && k1 - 15 >= 0) lr_back_group<L, false>(q, o, ln, k1, n, uw);
-        else lr_back_group<L, true>(q, o, ln, k1, n, uw);
-    };
-    LR_STAMP(img == 0, dbg, 2);
-    th_lgkm0();  // (the forward values are read back by this wave only: its own writes, in order)
-    float q = 0.0f;
-    LrBackOps Ab, Bb;
-    ld_back(0, Ab);
-    for (int cb = 0; cb < nch; cb++) {
-        for (int gg = 0; gg < G; gg += 2) {
-            const int gb = cb * G + gg;
-            if (gb >= ng) break;
-            if (gb + 1 < ng) ld_back(gb + 1, Bb);
-            back(gb, q, Ab);
-            if (gb + 1 >= ng) break;
-            if (gb + 2 < ng) ld_back(gb + 2, Ab);
-            back(gb + 1, q, Bb);
+        const int k = k1 - 4 * ln.step;  // (each sample clamped on its own: the mapping holds)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            A.t[e] = *(const float*)(Cq + (max(k - e, 0) * L + l) * 16 + 12);
+            A.x[e] = *(const float*)uaddr(max(k - e, 0));
         }
+        lr_back_group<L, true>(q, A, ln, k1, n, uaddr(max(k1 - 4 * ln.step, 0)));
+    };
+    float q = 0.0f;
+    for (int cb = 0; cb < nch; cb++) {
+        const int lo = max(cb * G, 1), hi = min(cb * G + G, ngf);  // whole back groups: 1 .. ngf - 1
+        if (cb == 0) back_guarded(0, q);
+        for (int b0 = lo; b0 < hi; b0 += UB) {
+            LrBackOps A, B;
+            ld_back(b0, A);
+#pragma unroll
+            for (int gg = 0; gg < UB; gg++) {
+                const int gb = b0 + gg;
+                LrBackOps& cur = gg & 1 ? B : A;
+                LrBackOps& nxt = gg & 1 ? A : B;
+                if (gg + 1 < UB) ld_back(gb + 1, nxt);
+                if (gb < hi) {
+                    const int k1 = n - 1 - 16 * gb;
+                    lr_back_group<L, false>(q, cur, ln, k1, n, uaddr(k1 - 4 * ln.step));
+                }
+            }
+        }
+        if (ng > ngf && ngf >= cb * G && ngf < cb * G + G && ngf >= 1) back_guarded(ngf, q);
         th_lgkm0();
         th_barrier();
     }

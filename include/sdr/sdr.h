@@ -239,7 +239,10 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_rig
                    int16_t* out, float* conf);
 /* cv::ximgproc::fastGlobalSmootherFilter(guide, src, dst, lambda, sigma, attenuation, iters) on
  * nimg float images [nimg][h][w] sharing one 8-bit guide, in place, async on `stream`; solver
- * SDR_FGS_PCR or SDR_FGS_THOMAS. */
+ * SDR_FGS_PCR or SDR_FGS_THOMAS.  SDR_FGS_THOMAS needs every pass's lambda * attenuation^k in
+ * [0, 2^100] and allocates (stream-ordered, per call) 4 * (6 + 10 * num_iter) bytes a sample of
+ * w x h rounded up to 4 each way: the coefficients of its 2 * num_iter passes (20 B a sample each)
+ * and the pass layouts. */
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
                           double lambda, double sigma_color, double lambda_attenuation,
                           int num_iter, float* d_img, int nimg, int solver, void* stream);

@@ -1003,15 +1003,13 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
     for (int c = 0; c < nch; c++) {
         if (c > 0) th_barrier();
         for (int b0 = c * G; b0 < min(c * G + G, ngf); b0 += UB) {
-            LrFwdOps A, B;
-            ld_fwd(b0, A);
+            LrFwdOps ops[UB];  // (one set per unrolled group: static indices, no copies)
+            ld_fwd(b0, ops[0]);
 #pragma unroll
             for (int gg = 0; gg < UB; gg++) {
                 const int g = b0 + gg;
-                LrFwdOps& cur = gg & 1 ? B : A;
-                LrFwdOps& nxt = gg & 1 ? A : B;
-                if (gg + 1 < UB) ld_fwd(g + 1, nxt);
-                if (g < ngf) lr_fwd_group<L, false>(p, cur, ln, 16 * g, n, uaddr(16 * g + 4 * ln.step));
+                if (gg + 1 < UB) ld_fwd(g + 1, ops[gg + 1 < UB ? gg + 1 : gg]);
+                if (g < ngf) lr_fwd_group<L, false>(p, ops[gg], ln, 16 * g, n, uaddr(16 * g + 4 * ln.step));
             }
         }
         if (ngf < ng && ngf >= c * G && ngf < c * G + G) {  // the partial last group is in this chunk
@@ -1053,17 +1051,15 @@ __device__ __forceinline__ void lr_solver(int n, int nch, int img, int lane, boo
         const int lo = max(cb * G, 1), hi = min(cb * G + G, ngf);  // whole back groups: 1 .. ngf - 1
         if (cb == 0) back_guarded(0, q);
         for (int b0 = lo; b0 < hi; b0 += UB) {
-            LrBackOps A, B;
-            ld_back(b0, A);
+            LrBackOps ops[UB];
+            ld_back(b0, ops[0]);
 #pragma unroll
             for (int gg = 0; gg < UB; gg++) {
                 const int gb = b0 + gg;
-                LrBackOps& cur = gg & 1 ? B : A;
-                LrBackOps& nxt = gg & 1 ? A : B;
-                if (gg + 1 < UB) ld_back(gb + 1, nxt);
+                if (gg + 1 < UB) ld_back(gb + 1, ops[gg + 1 < UB ? gg + 1 : gg]);
                 if (gb < hi) {
                     const int k1 = n - 1 - 16 * gb;
-                    lr_back_group<L, false>(q, cur, ln, k1, n, uaddr(k1 - 4 * ln.step));
+                    lr_back_group<L, false>(q, ops[gg], ln, k1, n, uaddr(k1 - 4 * ln.step));
                 }
             }
         }
@@ -1090,12 +1086,20 @@ __device__ __forceinline__ void lr_loader_writer(const FgsThArgs& a, size_t fofs
         th_issue<L, 16>(gc, a.st, l0, c * CH, 1, last, lds + kLrU + c * 16384, lw, lane);
     };
     int issued = 0;
+#ifdef SDR_LR_PRELOAD  // diagnostic: every chunk landed before the solvers start
+    for (; issued < nch; issued++) {
+        issue(issued);
+        th_vmcnt<0>();
+    }
+    for (int c = 0; c < nch; c++) th_barrier();
+#else
     for (; issued < min(kLrAhead, nch); issued++) issue(issued);
     for (int c = 0; c < nch; c++) {
         th_wait_chunks<IW>(issued - min(c + 2, issued));
         th_barrier();
         if (issued < nch) issue(issued++);
     }
+#endif
     // ---- writers ----
     const float2* R = (const float2*)lds;
     for (int cb = 0; cb < nch; cb++) {
@@ -1134,6 +1138,11 @@ __global__ __launch_bounds__(256) void k_fgs_lr(FgsThArgs a) {
     const int l0 = blockIdx.x * L;
     const int nch = (a.n + CH - 1) / CH;
     LR_STAMP(wave == 0, a.dbg, 0);
+#ifdef SDR_LR_ONE_SOLVER  // diagnostic: the second solver only keeps the barrier count (its image is not solved)
+    if (wave == 1) {
+        for (int c = 0; c < 2 * nch; c++) th_barrier();
+    } else
+#endif
     if (wave < 2) lr_solver<L>(a.n, nch, wave, lane, l0 + (lane & 15) < a.nl, lds, a.dbg);
     else lr_loader_writer<L>(a, fofs, l0, nch, wave - 2, lane, lds);
     LR_STAMP(wave == 2, a.dbg, 4);

@@ -110,7 +110,7 @@ def test_world2_bench_step_gather_loop():
     assert len(lines) == 1, res.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["steps"] == 6
-    assert out["gather_check"] == {"step": 7, "ranks": 2, "ok": True}
+    assert out["gather_check"] == {"step": 7, "ranks": 2, "gather_every": 8, "ok": True}
 
 
 def test_bench_gpus2_self_launch():

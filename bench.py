@@ -46,7 +46,11 @@ CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md chip table: max clock (the latency floors
 # (profiles/r5_streams_sweep.md): C2 is flat from 2 to 6 (1737-1772 fps); the class path's frame
 # (C4: ~30 short launches, the sequential FGS passes a few hundred workgroups each) fills the chip
 # only with more frames beside it, 2367 fps at 3 and 3592-3651 at 6
-STREAMS_DEFAULT = {"c4": 6}
+# frames in flight per config: C4's short launches fill the chip only with several frames beside
+# each other (profiles/r5_streams_sweep.md); C2 is flat from 2 to 6 in flight, and with RCCL's own
+# stream beside them 3 streams lost ~4.6 % of the rate against 1.4-1.8 % at 2
+# (profiles/r6_streams_c2/: the RCCL world-1 line against the plain one, two rounds on one box)
+STREAMS_DEFAULT = {"c4": 6, "c2": 2}
 
 CONFIGS = {
     "c2": ("C2 (BASELINE configs[1]): 1280x720 d=128 MODE_SGBM 5-path + reprojectImageTo3D(Q, "

@@ -524,6 +524,80 @@ __global__ __launch_bounds__(128) void k5(float* out, unsigned long long* t, int
     out[blockIdx.x * 128 + threadIdx.x] = uu[lane] + (float)(key & 1);
 }
 
+template <int KEY>
+__global__ __launch_bounds__(128) void k6(float* out, unsigned long long* t, int nw) {
+    constexpr int NP = N + 4, CP = N * 3 + 12;  // padded line strides: lanes on distinct banks
+    __shared__ __attribute__((aligned(16))) float cf[L * CP];  // [l][k/4][12]
+    __shared__ __attribute__((aligned(16))) float tt[L * NP];  // [l][k]
+    __shared__ __attribute__((aligned(16))) float u[2][L * NP];    // [l][k]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < L * N; i += blockDim.x) {
+        const int l = i / N, k = i % N;
+        const float den = 1.5f + (i & 7) * 0.1f;
+        float* c = cf + l * CP + (k / 4) * 12 + (k & 3);
+        c[0] = -0.2f - (i & 3) * 0.01f;
+        c[4] = den;
+        c[8] = 1.0f / den;
+        tt[l * NP + k] = 0.1f;
+        u[0][l * NP + k] = 0.7f + (i & 15) * 0.01f;
+        u[1][l * NP + k] = 0.3f + (i & 31) * 0.01f;
+    }
+    __syncthreads();
+    if (w >= nw) return;
+    float* uu = u[w];
+    const int l = lane & 15;
+    uint32_t key = ~0u;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime(), t1 = 0, t2 = 0;
+    float p = 0.0f;
+    const float4* U4 = (const float4*)(uu + l * NP);
+    float4* W4 = (float4*)(uu + l * NP);
+    const float4* C4 = (const float4*)(cf + l * CP);
+    const float4* T4 = (const float4*)(tt + l * NP);
+    float4 xa = U4[0], aa = C4[0], da = C4[1], ra = C4[2];
+#pragma unroll 4
+    for (int b = 0; b < N / 4; b++) {
+        const int bn = b + 1 < N / 4 ? b + 1 : b;
+        const float4 xn = U4[bn], an = C4[3 * bn], dn = C4[3 * bn + 1], rn = C4[3 * bn + 2];
+        float4 o;
+        const float xv[4] = {xa.x, xa.y, xa.z, xa.w}, av[4] = {aa.x, aa.y, aa.z, aa.w};
+        const float dv[4] = {da.x, da.y, da.z, da.w}, rv[4] = {ra.x, ra.y, ra.z, ra.w};
+        float ov[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const float x = xv[e] - av[e] * p;
+            const float q0 = x * rv[e];
+            p = __builtin_fmaf(-__builtin_fmaf(q0, dv[e], -x), rv[e], q0);
+            if (KEY) key = min(key, tkey(q0));
+            ov[e] = p;
+        }
+        o = make_float4(ov[0], ov[1], ov[2], ov[3]);
+        W4[b] = o;
+        xa = xn; aa = an; da = dn; ra = rn;
+    }
+    t1 = __builtin_amdgcn_s_memtime();
+    float4 xb = W4[N / 4 - 1], tb = T4[N / 4 - 1];
+#pragma unroll 4
+    for (int b = N / 4 - 1; b >= 0; b--) {
+        const int bn = b > 0 ? b - 1 : 0;
+        const float4 xn = W4[bn], tn = T4[bn];
+        const float xv[4] = {xb.x, xb.y, xb.z, xb.w}, tv[4] = {tb.x, tb.y, tb.z, tb.w};
+        float ov[4];
+#pragma unroll
+        for (int e = 3; e >= 0; e--) {
+            p = xv[e] - tv[e] * p;
+            ov[e] = p;
+        }
+        W4[b] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+        xb = xn; tb = tn;
+    }
+    t2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        t[(blockIdx.x * 2 + w) * 2] = t1 - t0;
+        t[(blockIdx.x * 2 + w) * 2 + 1] = t2 - t1;
+    }
+    out[blockIdx.x * 128 + threadIdx.x] = uu[lane] + (float)(key & 1);
+}
+
 template <int V, int KEY>
 void run(const char* name, int nw) {
     float* o;
@@ -535,6 +609,7 @@ void run(const char* name, int nw) {
         else if (V == 3) hipLaunchKernelGGL((k3<KEY>), dim3(64), dim3(128), 0, 0, o, t, nw);
         else if (V == 4) hipLaunchKernelGGL((k4<KEY>), dim3(64), dim3(128), 0, 0, o, t, nw);
         else if (V == 5) hipLaunchKernelGGL((k5<KEY>), dim3(64), dim3(128), 0, 0, o, t, nw);
+        else if (V == 6) hipLaunchKernelGGL((k6<KEY>), dim3(64), dim3(128), 0, 0, o, t, nw);
         else hipLaunchKernelGGL((k<V, KEY>), dim3(64), dim3(128), 0, 0, o, t, nw);
     }
     hipDeviceSynchronize();
@@ -564,6 +639,8 @@ int main() {
         run<4, 1>("V4 no exec masks, key", nw);
         run<5, 0>("V5 lane = line, line-major b128, no key", nw);
         run<5, 1>("V5 lane = line, line-major b128, key", nw);
+        run<6, 0>("V6 = V5 with padded line strides, no key", nw);
+        run<6, 1>("V6 = V5 with padded line strides, key", nw);
     }
     return 0;
 }

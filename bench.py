@@ -203,19 +203,21 @@ def load_traffic(kernel_tag):
 
 
 def stream_probe(dev, mib=2048, iters=20):
-    """This box's streaming rate (sdr_stream_probe: a copy with the path kernels' 16-byte loads and
-    non-temporal stores over 2 GiB, read + write bytes), the ceiling a bandwidth-bound kernel of
-    the same box can be held against: box-to-box spread shows up here and in `achieved` alike."""
+    """This box's streaming rates (sdr_stream_probe_ex over 2 GiB buffers, far beyond the 256 MiB
+    Infinity Cache): the fastest copy (read + write bytes), read-only and write-only.  A path kernel
+    reads and writes in about equal parts, so `gbs` (the copy) is its yardstick; box-to-box spread
+    shows up here and in `achieved` alike (profiles/r6_copy_rate.txt: 85 copy shapes on one box,
+    5.0-5.8 TB/s; reads 6.3-6.4)."""
     import ctypes
 
     from stereo_depth_ruler_amd._lib import check, lib
 
-    g = ctypes.c_double()
-    check(lib().sdr_stream_probe(dev.index, mib << 20, iters, ctypes.byref(g)))
-    return {"gbs": round(g.value, 1), "what": f"sdr_stream_probe: the fastest of 12 copy variants (4 or 8 "
-                                              f"16-B loads in flight per thread, plain or non-temporal "
-                                              f"stores, 4/8/16 workgroups a CU), {iters} copies of {mib} MiB "
-                                              f"each, read + write bytes"}
+    g = (ctypes.c_double * 3)()
+    check(lib().sdr_stream_probe_ex(dev.index, mib << 20, iters, g))
+    return {"gbs": round(g[0], 1), "read_gbs": round(g[1], 1), "write_gbs": round(g[2], 1),
+            "what": f"sdr_stream_probe_ex: the fastest of 16 copy shapes (4 or 8 16-B loads in flight per "
+                    f"thread, plain or non-temporal stores, 2/4/8/16 workgroups a CU), {iters} copies of "
+                    f"{mib} MiB each, read + write bytes; read-only and write-only beside"}
 
 
 def free_port() -> int:
@@ -795,6 +797,9 @@ def main():
                 hb["frac_of_probe"] = round(hb["achieved"] / probe["gbs"], 4)
             if a.hbm_only and kind == "sgbm" and mode == 0:
                 roofline["hbm_only"] = hbm_only_paths()
+                if a.stream_probe:
+                    roofline["hbm_only"]["frac_of_probe"] = round(roofline["hbm_only"]["achieved"] /
+                                                                  probe["gbs"], 4)
         m.enable_timing(0)
     pix = world * a.steps * batch * W * H
     value = pix / el / 1e6

@@ -436,10 +436,13 @@ int sdr_sgbm_debug_knob(sdr_sgbm* h, int knob, int value);
  * permlane swaps); fills 4 failure counters, all zero on a healthy gfx950. */
 int sdr_selftest_wave_ops(int* failures4);
 
-/* The device's streaming rate: `iters` back-to-back copies of a `bytes` buffer (16-byte loads,
- * non-temporal stores: the path kernels' read + write pattern), read + write bytes per second in
- * GB/s.  bench.py records it beside the dominant kernel's rate (box-to-box spread). */
+/* The device's streaming rate: `iters` back-to-back copies of a `bytes` buffer, the fastest of
+ * several access shapes (16-byte loads, 4 or 8 in flight per thread, plain or non-temporal
+ * stores, 2-16 workgroups a CU), read + write bytes per second in GB/s.  bench.py records it
+ * beside the dominant kernel's rate (box-to-box spread).  _ex fills gbs3 = {copy, read-only,
+ * write-only}. */
 int sdr_stream_probe(int device, size_t bytes, int iters, double* gbs);
+int sdr_stream_probe_ex(int device, size_t bytes, int iters, double* gbs3);
 
 /* Diagnostics: synchronously copy an internal buffer of the last compute to host memory.
  * stage 0 = cost volume C [F][H][W1][D] s16, 1 = WTA disparity before the LR check [F][H][W] s16,

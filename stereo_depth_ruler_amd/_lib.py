@@ -157,6 +157,7 @@ SIGNATURES = [
     ("sdr_sgbm_kernel_time", _i, [_vp, _i, _i, _c.POINTER(_c.c_float), _c.POINTER(_c.c_int)]),
     ("sdr_sgbm_last_status", _i, [_vp]),
     ("sdr_stream_probe", _i, [_i, _sz, _i, _c.POINTER(_c.c_double)]),
+    ("sdr_stream_probe_ex", _i, [_i, _sz, _i, _c.POINTER(_c.c_double)]),
     ("sdr_sgbm_debug_knob", _i, [_vp, _i, _i]),
     ("sdr_build_id", _c.c_char_p, []),
     ("sdr_last_error", _c.c_char_p, []),

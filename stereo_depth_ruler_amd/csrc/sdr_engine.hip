@@ -1526,6 +1526,15 @@ int sdr_stream_probe(int device, size_t bytes, int iters, double* gbs) {
     return sdr::stream_probe(bytes, iters, gbs) ? fail(SDR_ERR_NOMEM, "stream probe failed") : SDR_OK;
 }
 
+int sdr_stream_probe_ex(int device, size_t bytes, int iters, double* gbs3) {
+    if (!gbs3 || bytes < 16 || iters < 1) return fail(SDR_ERR_ARG, "bad argument");
+    int ndev = 0;
+    SDR_HIP(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SDR_ERR_DEVICE, "invalid device index");
+    SDR_HIP(hipSetDevice(device));
+    return sdr::stream_probe_ex(bytes, iters, gbs3) ? fail(SDR_ERR_NOMEM, "stream probe failed") : SDR_OK;
+}
+
 int sdr_selftest_wave_ops(int* failures4) {
     if (!failures4) return fail(SDR_ERR_ARG, "null argument");
     return sdr::selftest_wave_ops(failures4) ? fail(SDR_ERR_DEVICE, "selftest launch failed") : SDR_OK;

@@ -273,6 +273,7 @@ void launch_area_half(const uint8_t* src, int W, int H, size_t stride, uint8_t* 
                       size_t dstride, int F, hipStream_t st);
 int selftest_wave_ops(int* failures);
 int stream_probe(size_t bytes, int iters, double* gbs);
+int stream_probe_ex(size_t bytes, int iters, double* out3);
 
 // Per-kernel HIP-event timing of a matcher handle (timing level 2, sdr_sgbm_kernel_time): an
 // event pair of SDR_KERNEL_* kind `kind` on the handle's stream around one launch.  Kernels another

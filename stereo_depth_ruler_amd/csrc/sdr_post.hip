@@ -701,7 +701,40 @@ __global__ __launch_bounds__(256) void k_stream_probe(const probe_u32x4* __restr
     }
 }
 
+// read-only (an XOR of every vector, stored only if it matches an unlikely value) and write-only
+// forms of the same access shape: the box's HBM rates for the two directions
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_read(const probe_u32x4* __restrict__ src, probe_u32x4* __restrict__ dst,
+                                                     size_t n) {
+    const size_t span = (size_t)256 * U;
+    probe_u32x4 acc = {0u, 0u, 0u, 0u};
+    for (size_t base = (size_t)blockIdx.x * span; base + span <= n; base += (size_t)gridDim.x * span) {
+#pragma unroll
+        for (int u = 0; u < U; u++) acc ^= __builtin_nontemporal_load(&src[base + u * 256 + threadIdx.x]);
+    }
+    if (acc.x == 0x9E3779B9u && acc.y == 0x7F4A7C15u) dst[threadIdx.x] = acc;
+}
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_write(const probe_u32x4* __restrict__ src, probe_u32x4* __restrict__ dst,
+                                                      size_t n) {
+    const size_t span = (size_t)256 * U;
+    const probe_u32x4 v = {1u, 2u, 3u, (unsigned)blockIdx.x};
+    for (size_t base = (size_t)blockIdx.x * span; base + span <= n; base += (size_t)gridDim.x * span) {
+#pragma unroll
+        for (int u = 0; u < U; u++) dst[base + u * 256 + threadIdx.x] = v;
+    }
+}
+
+int stream_probe_ex(size_t bytes, int iters, double* out3);
 int stream_probe(size_t bytes, int iters, double* gbs) {
+    double r[3];
+    const int rc = stream_probe_ex(bytes, iters, r);
+    if (rc == 0) *gbs = r[0];
+    return rc;
+}
+
+// out3: the fastest copy (read + write bytes), read-only and write-only rates, GB/s
+int stream_probe_ex(size_t bytes, int iters, double* out3) {
     probe_u32x4 *a = nullptr, *b = nullptr;
     const size_t n = bytes / 16;
     if (hipMalloc((void**)&a, n * 16) != hipSuccess) return -1;
@@ -712,28 +745,33 @@ int stream_probe(size_t bytes, int iters, double* gbs) {
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int rc = -1;
-    double best = 0.0;
+    double best[3] = {0.0, 0.0, 0.0};
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
         hipEventCreate(&e1) == hipSuccess && hipMemsetAsync(a, 1, n * 16, st) == hipSuccess) {
         typedef void (*probe_fn)(const probe_u32x4*, probe_u32x4*, size_t);
-        const probe_fn fns[4] = {k_stream_probe<4, false>, k_stream_probe<4, true>, k_stream_probe<8, false>,
-                                 k_stream_probe<8, true>};
-        for (int wpc : {4, 8, 16})
-            for (probe_fn f : fns) {
+        // (kind 0: copy, 1: read, 2: write) -- the copy variants of profiles/r6_copy_rate.txt's best
+        const struct { probe_fn f; int kind; } fns[] = {
+            {k_stream_probe<4, false>, 0}, {k_stream_probe<4, true>, 0}, {k_stream_probe<8, false>, 0},
+            {k_stream_probe<8, true>, 0},  {k_stream_read<4>, 1},        {k_stream_read<8>, 1},
+            {k_stream_write<8>, 2}};
+        for (int wpc : {2, 4, 8, 16})
+            for (const auto& v : fns) {
                 const dim3 grid(device_cus() * wpc), blk(256);
-                hipLaunchKernelGGL(f, grid, blk, 0, st, a, b, n);  // warm
+                hipLaunchKernelGGL(v.f, grid, blk, 0, st, a, b, n);  // warm
                 (void)hipEventRecord(e0, st);
-                for (int i = 0; i < iters; i++) hipLaunchKernelGGL(f, grid, blk, 0, st, a, b, n);
+                for (int i = 0; i < iters; i++) hipLaunchKernelGGL(v.f, grid, blk, 0, st, a, b, n);
                 (void)hipEventRecord(e1, st);
                 float ms = 0.0f;
                 if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess &&
                     ms > 0.0f) {
-                    best = std::max(best, 2.0 * (double)(n * 16) * iters / (ms * 1e-3) / 1e9);
+                    const double by = (v.kind == 0 ? 2.0 : 1.0) * (double)(n * 16) * iters;
+                    best[v.kind] = std::max(best[v.kind], by / (ms * 1e-3) / 1e9);
                     rc = 0;
                 }
             }
     }
-    if (rc == 0) *gbs = best;
+    if (rc == 0)
+        for (int i = 0; i < 3; i++) out3[i] = best[i];
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (st) (void)hipStreamDestroy(st);

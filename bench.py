@@ -687,6 +687,10 @@ def main():
         avg_us = tot / cnt * 1e3
         samples = nmatch // 2 * batch * rw * rh  # line-samples one pass solves (both images together)
         coef = per_kind["fgs_coef"]
+        avg_us_corr = corr["fgs_pass"][0] / cnt * 1e3
+        # HBM bytes a pass moves by its data flow: per line-sample the two right-hand sides and the
+        # four coefficients read (8 + 16 B, the LDS images' chunk layout), the two results written
+        fgs_bytes = samples * (8 + 16 + 8)
         return {
             "bound": "latency",
             "kernel": "k_fgs_lr (sequential FGS pass, SDR_FGS_THOMAS: the lines resident in LDS, one solver "
@@ -696,11 +700,16 @@ def main():
             "peak": round(samples / (floor_us * 1e-6) / 1e9, 3),
             "unit": "G line-samples/s",
             "frac": round(floor_us / avg_us, 4),
-            "traffic": None,
+            "traffic": load_traffic(f"{a.config}:k_fgs_lr"),
+            "traffic_unit": "HBM bytes a launch (PMC, profiles/pmc_traffic.json); the pass is latency-bound",
+            "algorithmic_bytes_per_launch": fgs_bytes,
+            "bytes_model": "32 B a line-sample: 8 (two right-hand sides) + 16 (coefficients) read, 8 written",
             "model": (f"a pass = lines of a {rw}x{rh} ROI, mean chain {chain:.0f} samples (rows {rw}, columns "
                       f"{rh}); floor = chain x ({fwd_ops} fwd + {back_ops} back dependent ops) x {cyc_op} "
                       f"cycles at {CLOCK_GHZ} GHz = {floor_us:.2f} us a pass"),
             "avg_launch_us": round(avg_us, 2),
+            "avg_launch_us_overhead_corrected": round(avg_us_corr, 2),
+            "frac_overhead_corrected": round(floor_us / avg_us_corr, 4) if avg_us_corr > 0 else None,
             "floor_us": round(floor_us, 2),
             "measured_cycles_per_sample": round(avg_us * CLOCK_GHZ * 1e3 / chain, 1),
             "floor_cycles_per_sample": round((fwd_ops + back_ops) * cyc_op, 1),

@@ -20,9 +20,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -314,19 +316,55 @@ namespace {
             return sdr::set_error(SDR_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-// stream-ordered scratch freed on every exit path
-struct AsyncScratch {
+// The voxel grid's scratch: one grow-only device arena a call, leased from a list of idle arenas
+// and bump-allocated.  The call reports a count, so it synchronises its stream before it returns
+// and its arena goes back to the list idle (the lease synchronises again on an early exit).
+// Stream-ordered allocations freed at the end of every call measured 0.75-1.45 ms of host time
+// a call on MI355X (the hipFreeAsync calls), more than the grid's kernels take.
+struct Arena {
+    int dev = 0;
+    sdr::Buf buf;
+};
+std::mutex g_arena_mu;
+std::vector<Arena*> g_idle_arenas;
+
+struct ArenaLease {
     hipStream_t st;
-    std::vector<void*> ptrs;
-    explicit AsyncScratch(hipStream_t s) : st(s) {}
-    void* get(size_t bytes) {
-        void* p = nullptr;
-        if (hipMallocAsync(&p, bytes ? bytes : 1, st) != hipSuccess) return nullptr;
-        ptrs.push_back(p);
-        return p;
+    Arena* a = nullptr;
+    size_t used = 0;
+    explicit ArenaLease(hipStream_t s) : st(s) {}
+    // an idle arena of the stream's device with room for `bytes`: SDR_OK or an SDR_* status
+    int open(size_t bytes) {
+        int dev = 0;
+        const hipError_t e = st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev);
+        if (e != hipSuccess) return sdr::set_error(SDR_ERR_DEVICE, std::string("device of the stream: ") + hipGetErrorString(e));
+        {
+            std::lock_guard<std::mutex> lk(g_arena_mu);
+            for (size_t i = 0; i < g_idle_arenas.size(); i++) {
+                if (g_idle_arenas[i]->dev == dev) {
+                    a = g_idle_arenas[i];
+                    g_idle_arenas.erase(g_idle_arenas.begin() + i);
+                    break;
+                }
+            }
+        }
+        if (!a) {
+            a = new Arena;
+            a->dev = dev;
+        }
+        return sdr::ensure(a->buf, bytes);  // grows (hipFree + hipMalloc) only past its size
     }
-    ~AsyncScratch() {
-        for (void* p : ptrs) (void)hipFreeAsync(p, st);
+    void* get(size_t bytes) {
+        const size_t at = (used + 255) & ~(size_t)255;
+        if (!a || at + bytes > a->buf.n) return nullptr;
+        used = at + bytes;
+        return (char*)a->buf.p + at;
+    }
+    ~ArenaLease() {
+        if (!a) return;
+        (void)hipStreamSynchronize(st);  // idle before another call may take it
+        std::lock_guard<std::mutex> lk(g_arena_mu);
+        g_idle_arenas.push_back(a);
     }
 };
 
@@ -356,20 +394,52 @@ int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float
     if (n < 0) return sdr::set_error(SDR_ERR_ARG, "negative point count");
     if (!(lx > 0.0f) || !(ly > 0.0f) || !(lz > 0.0f)) return sdr::set_error(SDR_ERR_ARG, "leaf size must be > 0");
     hipStream_t st = (hipStream_t)stream;
+#ifdef SDR_VOXEL_TIMING  // diagnostic: host-side phase times of one call on stderr
+    struct Phases {
+        std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+        char buf[256];
+        int len = 0;
+        void mark(const char* what) {
+            const auto now = std::chrono::steady_clock::now();
+            len += std::snprintf(buf + len, sizeof(buf) - len, " %s %.1f", what,
+                                 std::chrono::duration<double, std::micro>(now - last).count());
+            last = now;
+        }
+        ~Phases() {
+            mark("end");
+            std::fprintf(stderr, "voxel_grid us:%s\n", buf);
+        }
+    } ph;
+#define VOXEL_MARK(w) ph.mark(w)
+#else
+#define VOXEL_MARK(w) (void)0
+#endif
     const float4* p = (const float4*)d_points;
     float4* out = (float4*)d_out;
     *out_count = 0;
     if (passthrough) *passthrough = 0;
     if (n == 0) return SDR_OK;
-    AsyncScratch scratch(st);
+    // the arena holds everything below: the min/max partials, then the keys, the sort's ping-pong
+    // (voxel, point) arrays, the heads and positions, the sort's histograms and the scan's totals
+    const size_t un = (size_t)n;
+    const int nb_rs = (n + sdr::kRsTile - 1) / sdr::kRsTile;
+    const int nh = 256 * nb_rs;
+    const int nb_scan = (std::max(n, nh) + sdr::kScanSeg - 1) / sdr::kScanSeg;
+    const size_t need = sizeof(float) * 7 * sdr::kMinMaxBlocks + un * (8 + 8 + 4 + 4 + 4 * 4) +
+                        sizeof(int) * ((size_t)nh + nb_scan) + 11 * 256;
+    ArenaLease scratch(st);
+    int rc = scratch.open(need);
+    if (rc) return rc;
     float* partial = (float*)scratch.get(sizeof(float) * 7 * sdr::kMinMaxBlocks);
-    if (!partial) return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+    if (!partial) return sdr::set_error(SDR_ERR_NOMEM, "scratch allocation failed");
     const int mmb = std::min(sdr::kMinMaxBlocks, (n + 255) / 256);
     hipLaunchKernelGGL(sdr::k_minmax, dim3(mmb), dim3(256), 0, st, p, n, partial);
     CLOUD_HIP(hipGetLastError());
     std::vector<float> hp((size_t)7 * mmb);
     CLOUD_HIP(hipMemcpyAsync(hp.data(), partial, sizeof(float) * hp.size(), hipMemcpyDeviceToHost, st));
+    VOXEL_MARK("mm_launch");
     CLOUD_HIP(hipStreamSynchronize(st));
+    VOXEL_MARK("mm_sync");
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     long long nfin = 0;
     for (int b = 0; b < mmb; b++) {
@@ -413,13 +483,11 @@ int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float
     // the sort's ping-pong (voxel, point) arrays and its histograms; the scan's block totals
     uint32_t* kv[4];
     for (auto& q : kv) q = (uint32_t*)scratch.get(sizeof(uint32_t) * n);
-    const int nb_rs = (n + sdr::kRsTile - 1) / sdr::kRsTile;
-    const int nh = 256 * nb_rs;
     int* hist = (int*)scratch.get(sizeof(int) * nh);
-    const int nb_scan = (std::max(n, nh) + sdr::kScanSeg - 1) / sdr::kScanSeg;
     int* spart = (int*)scratch.get(sizeof(int) * nb_scan);
     if (!keys || !sorted || !head || !pos || !kv[0] || !kv[1] || !kv[2] || !kv[3] || !hist || !spart)
-        return sdr::set_error(SDR_ERR_NOMEM, "hipMallocAsync failed");
+        return sdr::set_error(SDR_ERR_NOMEM, "scratch allocation failed");
+    VOXEL_MARK("alloc");
     const dim3 grid((n + 255) / 256);
     auto scan = [&](const int* in, int m, int* o) {
         const int nb = (m + sdr::kScanSeg - 1) / sdr::kScanSeg;
@@ -448,10 +516,13 @@ int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float
     scan(head, n, pos);
     hipLaunchKernelGGL(sdr::k_voxel_centroid, grid, dim3(256), 0, st, p, sorted, n, head, pos, out);
     CLOUD_HIP(hipGetLastError());
+    VOXEL_MARK("launches");
     int last_pos = 0, last_head = 0;
     CLOUD_HIP(hipMemcpyAsync(&last_pos, pos + n - 1, 4, hipMemcpyDeviceToHost, st));
     CLOUD_HIP(hipMemcpyAsync(&last_head, head + n - 1, 4, hipMemcpyDeviceToHost, st));
+    VOXEL_MARK("copies");
     CLOUD_HIP(hipStreamSynchronize(st));
+    VOXEL_MARK("sync");
     *out_count = last_pos + last_head;
     return SDR_OK;
 }

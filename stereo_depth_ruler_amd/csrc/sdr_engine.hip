@@ -178,6 +178,39 @@ int sdr::ensure(Buf& b, size_t bytes) {
     return SDR_OK;
 }
 
+hipError_t sdr::scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<int, hipMemPool_t> pools;
+    int dev = 0;
+    hipError_t e = st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemPool_t pool = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = pools.find(dev);
+        if (it == pools.end()) {
+            hipMemPoolProps props = {};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            e = hipMemPoolCreate(&pool, &props);
+            if (e != hipSuccess) return e;
+            uint64_t keep = UINT64_MAX;
+            e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            if (e != hipSuccess) {
+                (void)hipMemPoolDestroy(pool);
+                return e;
+            }
+            pools[dev] = pool;  // lives as long as the process
+        } else {
+            pool = it->second;
+        }
+    }
+    return hipMallocFromPoolAsync(p, bytes, pool, st);
+}
+
+hipError_t sdr::scratch_free(void* p, hipStream_t st) { return hipFreeAsync(p, st); }
+
 namespace {
 // Page-locked staging for the host-pointer entry points, kept by its owner across calls (no
 // allocation per call).  Copies go through it in row chunks of about kXferChunk bytes: on the way
@@ -1150,10 +1183,10 @@ int sdr_reproject_device(const float* d_disp, int W, int H, size_t disp_stride, 
     if (rc) return rc;
     if (xyz_stride < (size_t)W * 3) return fail(SDR_ERR_ARG, "xyz_stride < 3*width");
     int* mins = nullptr;
-    if (handle_missing) SDR_HIP(hipMallocAsync((void**)&mins, F * sizeof(int), (hipStream_t)stream));
+    if (handle_missing) SDR_HIP(sdr::scratch_alloc((void**)&mins, F * sizeof(int), (hipStream_t)stream));
     sdr::launch_reproject_f32(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,
                               d_xyz, xyz_stride, xyz_stride * H, F, (hipStream_t)stream);
-    if (mins) SDR_HIP(hipFreeAsync(mins, (hipStream_t)stream));
+    if (mins) SDR_HIP(sdr::scratch_free(mins, (hipStream_t)stream));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -1168,10 +1201,10 @@ int sdr_filter_speckles_device(int16_t* d_img, int W, int H, int F, int newVal, 
     hipStream_t st = (hipStream_t)stream;
     const size_t n = (size_t)F * W * H;
     int* scratch = nullptr;
-    SDR_HIP(hipMallocAsync((void**)&scratch, n * 8, st));
+    SDR_HIP(sdr::scratch_alloc((void**)&scratch, n * 8, st));
     sdr::launch_speckle(d_img, d_img, W, H, F, newVal, maxSpeckleSize, maxDiff, scratch, scratch + n,
                         nullptr, st);
-    SDR_HIP(hipFreeAsync(scratch, st));
+    SDR_HIP(sdr::scratch_free(scratch, st));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }
@@ -1188,12 +1221,12 @@ int sdr_disp16_reproject_device(const int16_t* d_disp, int W, int H, size_t disp
     int* mins = nullptr;
     hipStream_t st = (hipStream_t)stream;
     if (handle_missing) {
-        SDR_HIP(hipMallocAsync((void**)&mins, F * sdr::kMinSlots * sizeof(int), st));
+        SDR_HIP(sdr::scratch_alloc((void**)&mins, F * sdr::kMinSlots * sizeof(int), st));
         sdr::launch_min_s16(d_disp, (size_t)W * H, disp_stride * H, F, mins, st);
     }
     sdr::launch_reproject_s16(d_disp, W, H, disp_stride, disp_stride * H, Q, handle_missing, mins,
                               d_xyz, xyz_stride, xyz_stride * H, F, st);
-    if (mins) SDR_HIP(hipFreeAsync(mins, st));
+    if (mins) SDR_HIP(sdr::scratch_free(mins, st));
     SDR_HIP(hipGetLastError());
     return SDR_OK;
 }

@@ -23,6 +23,14 @@ struct Buf {
     size_t n = 0;
 };
 int ensure(Buf& b, size_t bytes);
+// Stream-ordered scratch of the one-shot device calls that do not synchronise (reprojection
+// minima, speckle labels, the FGS filter's coefficients) from a memory pool the library owns, one
+// a device, that keeps what it has mapped (release threshold: never; HIP's default pool returns
+// freed memory at each synchronize).  The voxel grid, which synchronises, leases a grow-only
+// arena instead (sdr_cloud.hip): its ~11 stream-ordered frees a call took 0.75-1.45 ms of host
+// time even from this pool.
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st);
+hipError_t scratch_free(void* p, hipStream_t st);
 // Records msg as the thread's sdr_last_error() and returns code.
 int set_error(int code, const std::string& msg);
 

@@ -2169,12 +2169,12 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
     const size_t px = (size_t)w * h;
     // (frames of the sequential solver's padded layouts: fgs_pad4(w) * fgs_pad4(h) >= px samples)
     const size_t fp = (size_t)sdr::fgs_pad4(w) * sdr::fgs_pad4(h);
-    WLS_HIP(hipMallocAsync((void**)&dlut, sizeof(float) * lut.size(), st));
+    WLS_HIP(sdr::scratch_alloc((void**)&dlut, sizeof(float) * lut.size(), st));
     // (FgsScratch: the sequential solver's two interleaved pass layouts, the weights, and 5 floats
     // a sample for each of its 2 * iters passes' coefficients; its loaders read up to
     // kFgsOverread bytes past an array)
     const size_t ncoef = solver == SDR_FGS_THOMAS ? (size_t)5 * (2 * iters) : 0;
-    WLS_HIP(hipMallocAsync((void**)&scr, sizeof(float) * fp * (6 + ncoef) + sdr::kFgsOverread, st));
+    WLS_HIP(sdr::scratch_alloc((void**)&scr, sizeof(float) * fp * (6 + ncoef) + sdr::kFgsOverread, st));
     WLS_HIP(hipMemcpyAsync(dlut, lut.data(), sizeof(float) * lut.size(), hipMemcpyHostToDevice, st));
     const sdr::FgsScratch fs{scr, scr + 2 * fp, scr + 4 * fp, scr + 5 * fp, scr + 6 * fp};
     // images are filtered in pairs (two right-hand sides of one system per line)
@@ -2184,8 +2184,8 @@ int sdr_fgs_filter_device(const uint8_t* d_guide, size_t gstride, int w, int h, 
                               w, h, 1, lambda, att, iters, solver, fs, st);
     }
     WLS_HIP(hipGetLastError());
-    WLS_HIP(hipFreeAsync(dlut, st));
-    WLS_HIP(hipFreeAsync(scr, st));
+    WLS_HIP(sdr::scratch_free(dlut, st));
+    WLS_HIP(sdr::scratch_free(scr, st));
     // the host LUT vector dies here: wait for its upload before returning
     WLS_HIP(hipStreamSynchronize(st));
     return SDR_OK;

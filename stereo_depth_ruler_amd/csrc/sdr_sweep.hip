@@ -181,7 +181,7 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
     auto col = [&](int m) { return x0w + r * M + m; };
     auto inside = [&](int m) { const int x = col(m); return x >= 0 && x < W1; };
     // ring entries of tile t, side (0: its first NCH columns' diagonal B, 1: its last NCH
-    // columns' diagonal A), parity: [NCH columns][16 lanes][DW words], then [NCH][16] deltas
+    // columns' diagonal A), parity: [NCH columns][DW words][16 lanes], then [NCH][16] deltas
     constexpr int EW = NCH * 16 * (DW + 1);
     auto entry = [&](int t, int side, int par) {
         return a.edge + ((((size_t)slot * a.ntiles + t) * 2 + side) * 2 + par) * EW;
@@ -236,17 +236,28 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
                 if (pub0 < 0 && pub1 < 0) return;
                 const int side = pub0 >= 0 ? 0 : 1, p = pub0 >= 0 ? pub0 : pub1;
                 if (data) {
+                    // word i of the 16 lanes of a column are 64 contiguous bytes ([column][word]
+                    // [lane]): each agent-scope store below (sc1: written through this XCD's L2)
+                    // fills whole 64-byte segments.  With a lane's words contiguous ([column][lane]
+                    // [word]) each 4-byte store cost a 32-byte memory write: 6 GB of a C3 batch's
+                    // down pass, 3 GB of its up pass
+                    // (the side is a constant in each branch: a runtime select between La and Lb
+                    // became a select of their addresses, which put both arrays in scratch)
                     uint32_t* e = entry(tile, side, (count / RS) & 1);
+                    auto put = [&](const uint32_t(&L)[M][DW], const uint32_t(&dl)[M]) __attribute__((always_inline)) {
 #pragma unroll
-                    for (int m = 0; m < MO; m++) {
-                        const int c = p * NCO + r * MO + m;  // column within the edge group
+                        for (int m = 0; m < MO; m++) {
+                            const int c = p * NCO + r * MO + m;  // column within the edge group
 #pragma unroll
-                        for (int i = 0; i < DW; i++)
-                            __hip_atomic_store(e + (c * 16 + gl) * DW + i, side ? La[m][i] : Lb[m][i],
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(e + NCH * 16 * DW + c * 16 + gl, side ? da[m] : db[m], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    }
+                            for (int i = 0; i < DW; i++)
+                                __hip_atomic_store(e + (c * DW + i) * 16 + gl, L[m][i], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(e + NCH * 16 * DW + c * 16 + gl, dl[m], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    };
+                    if (side) put(La, da);
+                    else put(Lb, db);
                 }
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no compiler motion across the wait
                 __builtin_amdgcn_s_waitcnt(0);
@@ -274,7 +285,7 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
                     const int cb = ROLE == kLeftHalo ? max(r * MH - 1, 0) : min(r * MH + MH, NCH - 1);
 #pragma unroll
                     for (int i = 0; i < DW; i++)
-                        rin[i] = __hip_atomic_load(e + (cb * 16 + gl) * DW + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        rin[i] = __hip_atomic_load(e + (cb * DW + i) * 16 + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     rdin = __hip_atomic_load(e + NCH * 16 * DW + cb * 16 + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     reloaded = true;
                 }
@@ -284,7 +295,7 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
                     uint32_t v[DW];
 #pragma unroll
                     for (int i = 0; i < DW; i++)
-                        v[i] = __hip_atomic_load(e + (c * 16 + gl) * DW + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        v[i] = __hip_atomic_load(e + (c * DW + i) * 16 + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const uint32_t dd =
                         __hip_atomic_load(e + NCH * 16 * DW + c * 16 + gl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll

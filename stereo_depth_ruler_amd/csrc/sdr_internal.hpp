@@ -162,6 +162,7 @@ struct SweepArgs {
     int ntiles, nslots;    // frames in flight = nslots (workgroups = nslots * ntiles, all resident)
     int up;
     int spin;              // polls before a wait gives up (kSweepSpin; lower through a debug knob)
+    int xcd;               // 1: a frame's consecutive tiles on one XCD (launch_sweep sets it)
 };
 // the down pass's WTA (A.8): the E, W, up records it reads and the outputs k_south_wta would write
 struct SweepWta {

@@ -38,6 +38,7 @@
 #include "sdr_internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sdr {
 
@@ -45,6 +46,7 @@ namespace {
 
 constexpr int kDppRowShr1 = 0x111;  // lane i <- lane i-1 within its 16-lane row
 constexpr int kDppRowShl1 = 0x101;  // lane i <- lane i+1 within its 16-lane row
+constexpr int kSweepXcds = 8;       // MI355X: blocks are dealt round-robin over 8 XCDs
 
 // slots (columns per lane row) of the own waves and the halo waves of a pass
 #ifndef SDR_SW_UP_MO
@@ -577,7 +579,14 @@ template <int DW, bool PAD, bool UP>
 __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep16(Geometry g, SweepArgs a, SweepWta w, int F) {
     __shared__ SweepLds<DW, UP> sh;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int slot = blockIdx.x / a.ntiles, tile = blockIdx.x - slot * a.ntiles;
+    // a.xcd (a measured A/B, off by default): blocks b and b + 8 share an XCD (its L2), so
+    // consecutive tiles of a frame at b, b + 8, ... read a halo's C columns from the L2 the
+    // neighbour filled.  The ring protocol assumes no placement either way.  The grid is a multiple
+    // of kSweepXcds (launch_sweep); the padding blocks exit at once.
+    const int lid = a.xcd ? (int)(blockIdx.x % kSweepXcds) * (int)(gridDim.x / kSweepXcds) + (int)(blockIdx.x / kSweepXcds)
+                          : (int)blockIdx.x;
+    if (lid >= a.nslots * a.ntiles) return;
+    const int slot = lid / a.ntiles, tile = lid - slot * a.ntiles;
     if (wv == 0) sweep_wave<DW, PAD, UP, kLeftHalo>(g, a, w, F, sh, wv, slot, tile);
     else if (wv == kSweepWaves - 1) sweep_wave<DW, PAD, UP, kRightHalo>(g, a, w, F, sh, wv, slot, tile);
     else sweep_wave<DW, PAD, UP, kOwn>(g, a, w, F, sh, wv, slot, tile);
@@ -622,8 +631,15 @@ SweepShape sweep_shape(const Geometry& g, int F, bool up) {
     return sh;
 }
 
-void launch_sweep(const Geometry& g, const SweepArgs& a, const SweepWta& w, int F, hipStream_t st) {
-    const dim3 grid(a.nslots * a.ntiles), block(64 * kSweepWaves);
+void launch_sweep(const Geometry& g, const SweepArgs& a0, const SweepWta& w, int F, hipStream_t st) {
+    // measured (profiles/r6_sweep_xcd_ab.txt): the XCD-grouped tiles cut the halos' HBM re-reads
+    // (C3 down 55.3 -> 50.9 GB, up 27.6 -> 25.9) but run slower (down 10.65 -> 11.67 ms, up 5.66 ->
+    // 6.55): a frame's tiles walk its rows in lockstep, so one XCD's demand comes in bursts where
+    // the linear order mixes frames at different rows.  Off unless SDR_SWEEP_XCD=1.
+    static const int xcd = getenv("SDR_SWEEP_XCD") ? atoi(getenv("SDR_SWEEP_XCD")) : 0;
+    SweepArgs a = a0;
+    a.xcd = xcd;
+    const dim3 grid((a.nslots * a.ntiles + kSweepXcds - 1) / kSweepXcds * kSweepXcds), block(64 * kSweepWaves);
 #define SDR_SWEEP(DW, PAD)                                                                          \
     if (a.up) hipLaunchKernelGGL((k_sweep16<DW, PAD, true>), grid, block, 0, st, g, a, w, F);       \
     else hipLaunchKernelGGL((k_sweep16<DW, PAD, false>), grid, block, 0, st, g, a, w, F);

@@ -579,12 +579,15 @@ template <int DW, bool PAD, bool UP>
 __global__ __launch_bounds__(64 * kSweepWaves) void k_sweep16(Geometry g, SweepArgs a, SweepWta w, int F) {
     __shared__ SweepLds<DW, UP> sh;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // a.xcd (a measured A/B, off by default): blocks b and b + 8 share an XCD (its L2), so
-    // consecutive tiles of a frame at b, b + 8, ... read a halo's C columns from the L2 the
-    // neighbour filled.  The ring protocol assumes no placement either way.  The grid is a multiple
-    // of kSweepXcds (launch_sweep); the padding blocks exit at once.
-    const int lid = a.xcd ? (int)(blockIdx.x % kSweepXcds) * (int)(gridDim.x / kSweepXcds) + (int)(blockIdx.x / kSweepXcds)
-                          : (int)blockIdx.x;
+    // blocks b and b + 8 share an XCD (its L2): two neighbouring tiles there read the C columns of
+    // each other's halo from the L2 the other filled.  For speed only: the ring protocol assumes
+    // no placement.  The grid is a multiple of 2 * kSweepXcds; the padding blocks exit at once.
+    const int b = (int)blockIdx.x;
+    // 1: tile t at blocks b, b + 8, ... of one XCD; 2: tiles 2j and 2j + 1 on one XCD (blocks b and
+    // b + 8), the pairs dealt round-robin (the grid is a multiple of 2 * kSweepXcds); 0: linear
+    const int lid = a.xcd == 1   ? (b % kSweepXcds) * (int)(gridDim.x / kSweepXcds) + b / kSweepXcds
+                    : a.xcd == 2 ? ((b / (2 * kSweepXcds)) * kSweepXcds + b % kSweepXcds) * 2 + (b / kSweepXcds) % 2
+                                 : b;
     if (lid >= a.nslots * a.ntiles) return;
     const int slot = lid / a.ntiles, tile = lid - slot * a.ntiles;
     if (wv == 0) sweep_wave<DW, PAD, UP, kLeftHalo>(g, a, w, F, sh, wv, slot, tile);
@@ -632,14 +635,15 @@ SweepShape sweep_shape(const Geometry& g, int F, bool up) {
 }
 
 void launch_sweep(const Geometry& g, const SweepArgs& a0, const SweepWta& w, int F, hipStream_t st) {
-    // measured (profiles/r6_sweep_xcd_ab.txt): the XCD-grouped tiles cut the halos' HBM re-reads
-    // (C3 down 55.3 -> 50.9 GB, up 27.6 -> 25.9) but run slower (down 10.65 -> 11.67 ms, up 5.66 ->
-    // 6.55): a frame's tiles walk its rows in lockstep, so one XCD's demand comes in bursts where
-    // the linear order mixes frames at different rows.  Off unless SDR_SWEEP_XCD=1.
-    static const int xcd = getenv("SDR_SWEEP_XCD") ? atoi(getenv("SDR_SWEEP_XCD")) : 0;
+    // tile -> XCD (profiles/r6_sweep_xcd_ab.txt, one box each; C3 PMC a 32-frame batch, algorithmic
+    // down 48.3 GB, up 24.2): linear (0) 55.3 / 27.6 GB, down 10.65 ms, up 5.66; a frame's tiles on
+    // one XCD (1) 50.9 / 25.9 GB but down 11.67, up 6.55 ms -- its tiles walk the rows in lockstep,
+    // so one XCD's demand comes in bursts where the other orders mix frames at different rows;
+    // pairs of tiles on one XCD (2, the default) 52.9 / 26.5 GB (1.10x) at the linear order's times
+    static const int xcd = getenv("SDR_SWEEP_XCD") ? atoi(getenv("SDR_SWEEP_XCD")) : 2;
     SweepArgs a = a0;
     a.xcd = xcd;
-    const dim3 grid((a.nslots * a.ntiles + kSweepXcds - 1) / kSweepXcds * kSweepXcds), block(64 * kSweepWaves);
+    const dim3 grid((a.nslots * a.ntiles + 2 * kSweepXcds - 1) / (2 * kSweepXcds) * (2 * kSweepXcds)), block(64 * kSweepWaves);
 #define SDR_SWEEP(DW, PAD)                                                                          \
     if (a.up) hipLaunchKernelGGL((k_sweep16<DW, PAD, true>), grid, block, 0, st, g, a, w, F);       \
     else hipLaunchKernelGGL((k_sweep16<DW, PAD, false>), grid, block, 0, st, g, a, w, F);

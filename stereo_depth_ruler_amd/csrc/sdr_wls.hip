@@ -252,6 +252,7 @@ struct FgsCoefJob {
     int nl, n;
     int st;           // k-major sample stride (nl rounded up to 4)
     int blocks;
+    int lpb;          // k_fgs_lrjob: lines a workgroup (16, 8 or 4)
 };
 
 struct FgsThArgs {
@@ -962,6 +963,25 @@ __device__ unsigned long long g_lr_blk[16][512][8];
     } while (0)
 #endif
 
+#ifdef SDR_TH_STAMPS
+// diagnostic build only: k_fgs_lrjob's per-workgroup stamps of the last launch (frame 0, the first
+// 512 workgroups; scripts/lj_stamps.py): 0 entry, 1 chunk 0 prepared (prep), 2 solver past its
+// first barrier, 3 solver done, 4 writer 0 done, 5 prep done, 6 / 7 s_memrealtime at 0 / 3
+__device__ unsigned long long g_lj_blk[512][8];
+#define LJ_STAMP(cond, i)                                                                            \
+    do {                                                                                             \
+        if ((cond) && (threadIdx.x & 63) == 0 && blockIdx.x < 512 && blockIdx.y == 0) {              \
+            g_lj_blk[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                                  \
+            if ((i) == 0) g_lj_blk[blockIdx.x][6] = __builtin_amdgcn_s_memrealtime();                 \
+            if ((i) == 3) g_lj_blk[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();                 \
+        }                                                                                            \
+    } while (0)
+#else
+#define LJ_STAMP(cond, i) \
+    do {                  \
+    } while (0)
+#endif
+
 // The solver wave of image `img` (0: A / U.x, 1: B / U.y).  The whole groups of a chunk run in
 // unrolled blocks of up to 8 with the next group's operands loaded during the current one into a
 // second, static register set (a loop-carried pair made the compiler copy the loads and wait for
@@ -1147,6 +1167,230 @@ __global__ __launch_bounds__(256) void k_fgs_lr(FgsThArgs a) {
     else lr_loader_writer<L>(a, fofs, l0, nch, wave - 2, lane, lds);
     LR_STAMP(wave == 2, a.dbg, 4);
     LR_STAMP(wave == 0, a.dbg, 5);
+}
+
+// ---- k_fgs_lrjob: the coefficient jobs the k_fgs_lr way (round 6) --------------------------
+// th_job_solver's recurrence, operations and roundings (bit-exact): per sample k of a line
+//   aa = lam * C[k-1] (C[-1] = 0),  cc = lam * C[k],  den = (1 - cc) - aa * (1 + t),
+//   r = fgs_rcp(den),  t = cc / den (from r by Markstein, or IEEE in a group holding a tiny cc)
+// with t carried from sample to sample: a chain of 9 dependent operations.  On one wave every
+// instruction it issues is on that chain (k_fgs_lr's finding), so the work is split so that the
+// chain's wave issues little else:
+//   wave 0     the solver: lane = (row, line) as in k_fgs_lr -- 4 consecutive samples x L lines
+//              an LDS instruction, the chain walking the rows by permlane swaps -- reading each
+//              sample's (aa, cc, 1 - cc) and writing (den, 1/den, t) with its row's stores
+//              (exec-masked per walk step, no selects; the writers add aa);
+//   wave 1     the prep wave: the line's weights DMA'd at the start (resident, kLrChunks chunks),
+//              then per chunk (aa, cc, 1 - cc) into LDS and a flag bit per 16-sample group holding a
+//              tiny cc (one word a chunk, read once by the solver) (0 < |cc| < 2^-96 (1 + 2 lam), where the reciprocal form may round apart
+//              from the division), a chunk ahead of the solver;
+//   waves 2, 3 the writers: chunk c's rows to coef and tt, a chunk behind the solver.
+// Iteration i (a barrier each, nch + 2 of them): prep chunk i, solve chunk i - 1, write chunk i - 2.
+// LDS: [weights: kLrChunks x 4 KiB][prep: kLrChunks x 16 KiB][rows: 2 x 16 KiB][chunk flags].
+constexpr int kLjW = kLrChunks * 4096, kLjP = kLrChunks * 16384, kLjO = 2 * 16384;
+constexpr int kLjLds = kLjW + kLjP + kLjO + kLrChunks * 4;  // + a flag word a chunk (bit: group)
+static_assert(1024 / 4 / 16 <= 32, "a chunk's groups fit a flag word");
+static_assert(kLjLds <= 160 * 1024, "one workgroup's LDS");
+
+// one walk step after another: the step-s row's 4 samples are the chain's, its stores the only
+// ones that land (the other rows compute from their own operands and are masked off)
+template <int L, bool EXACT, bool GUARD>
+__device__ __forceinline__ void lj_body(float& t, const float4 (&q)[4], int step, int k0, int n, float4* orow) {
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+        float3 res[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            if (!GUARD || k0 + 4 * s + e < n) {
+                const float aa = q[e].x, cc = q[e].y;
+#ifdef SDR_LJ_NOCHAIN  // diagnostic: one op a sample instead of the chain (results wrong)
+                t = t + cc;
+                res[e] = make_float3(aa, cc, t);
+                continue;
+#endif
+                const float den = q[e].z - aa * (1.0f + t);
+                const float r = fgs_rcp(den);
+                if constexpr (EXACT) {
+                    t = cc / den;
+                } else {
+                    const float q0 = cc * r;
+                    t = __builtin_fmaf(-__builtin_fmaf(q0, den, -cc), r, q0);  // cc / den
+                }
+                res[e] = make_float3(den, r, t);
+            }
+        }
+#ifndef SDR_LJ_NOSTORE  // diagnostic: the solver stores nothing (results wrong)
+        if (step == s) {
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if (!GUARD || k0 + 4 * s + e < n) *(float3*)(orow + e * L) = res[e];
+        }
+#else
+        if (t == 12345.0f) *(float3*)orow = res[0];
+#endif
+        t = lr_row(s, t);
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void lj_solver(int n, int nch, int lane, char* lds) {
+    constexpr int CH = 1024 / L, G = CH / 16;
+    constexpr int UB = G < 8 ? G : 8;  // groups an unrolled block (within a chunk)
+    const int row = lane >> 4, lq = lane & 15;
+    const int l = lq < L ? lq : L - 1;  // (lanes past L repeat line L - 1: the same values, the same slots)
+    const int step = row == 0 ? 0 : row == 1 ? 1 : row == 3 ? 2 : 3;
+    const float4* P = (const float4*)(lds + kLjW);
+    float4* O = (float4*)(lds + kLjW + kLjP);
+    const uint32_t* flags = (const uint32_t*)(lds + kLjW + kLjP + kLjO);
+    const int ng = (n + 15) / 16, ngf = n / 16;
+    struct Ops {
+        float4 q[4];
+    };
+    // a group's operands (every slot of a chunk holds a value: the prep wave covers all)
+    auto ld = [&](int g, Ops& o) __attribute__((always_inline)) {
+        const int k = 16 * g + 4 * step;
+#pragma unroll
+        for (int e = 0; e < 4; e++) o.q[e] = P[(k + e) * L + l];
+    };
+    uint32_t cflags = 0;  // the chunk's group flags (bit g - c * G), wave-uniform
+    auto group = [&](float& t, const Ops& o, int g, int c, auto guard) __attribute__((always_inline)) {
+        constexpr bool GU = decltype(guard)::value;
+        float4* orow = O + (c & 1) * 1024 + (16 * g - c * CH + 4 * step) * L + l;
+        if ((cflags >> (g - c * G)) & 1u) lj_body<L, true, GU>(t, o.q, step, 16 * g, n, orow);
+        else lj_body<L, false, GU>(t, o.q, step, 16 * g, n, orow);
+    };
+    float t = 0.0f;
+    th_barrier();  // iteration 0: chunk 0 prepared
+    LJ_STAMP(true, 2);
+    for (int c = 0; c < nch; c++) {
+        cflags = __builtin_amdgcn_readfirstlane(flags[c]);
+        for (int b0 = c * G; b0 < min(c * G + G, ngf); b0 += UB) {
+            Ops ops[UB];  // (one set per unrolled group: static indices, no copies)
+            ld(b0, ops[0]);
+#pragma unroll
+            for (int gg = 0; gg < UB; gg++) {
+                const int g = b0 + gg;
+                if (gg + 1 < UB) ld(g + 1, ops[gg + 1 < UB ? gg + 1 : gg]);
+                if (g < ngf) group(t, ops[gg], g, c, std::false_type{});
+            }
+        }
+        if (ngf < ng && ngf >= c * G && ngf < c * G + G) {  // the line's partial last group
+            Ops o;
+            ld(ngf, o);
+            group(t, o, ngf, c, std::true_type{});
+        }
+        th_lgkm0();
+        th_barrier();
+    }
+    LJ_STAMP(true, 3);
+    th_barrier();  // iteration nch + 1: the writers' last chunk
+}
+
+// s_waitcnt for the prep wave's DMA: chunk i landed when at most `younger` chunks (4
+// wave-instructions each) are in flight after it
+__device__ __forceinline__ void lj_wait(int younger) {
+    static_assert(kLrChunks <= 6, "vmcnt cases");
+    switch (younger) {
+        case 0: th_vmcnt<0>(); break;
+        case 1: th_vmcnt<4>(); break;
+        case 2: th_vmcnt<8>(); break;
+        case 3: th_vmcnt<12>(); break;
+        case 4: th_vmcnt<16>(); break;
+        default: th_vmcnt<20>(); break;
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void lj_prep(const FgsCoefJob& J, size_t fofs, int l0, int nch, int lane, char* lds) {
+    constexpr int CH = 1024 / L;
+    const int last = J.n - 1;
+    const float lam = J.lam, tiny = 0x1p-96f * (1.0f + 2.0f * lam);
+    const float* W = (const float*)lds;
+    float4* P = (float4*)(lds + kLjW);
+    uint32_t* flags = (uint32_t*)(lds + kLjW + kLjP + kLjO);
+    if (lane < kLrChunks) flags[lane] = 0;
+    const char* gw = (const char*)(J.Cw + fofs);
+    for (int c = 0; c < nch; c++) {
+        th_issue<L, 4>(gw, J.st, l0, c * CH, 1, last, lds + c * 4096, 0, lane);
+        th_issue<L, 4>(gw, J.st, l0, c * CH, 1, last, lds + c * 4096, 1, lane);
+    }
+    for (int i = 0; i < nch + 2; i++) {
+        if (i < nch) {
+            lj_wait(nch - 1 - i);
+#pragma unroll 4
+            for (int it = 0; it < 16; it++) {
+                const int j = i * 1024 + it * 64 + lane;  // = k * L + l
+                const int k = j / L, l = j % L;
+                const float cw = W[j];
+                const float cp = k > 0 ? W[j - L] : 0.0f;
+                const float aa = lam * cp, cc = lam * cw;
+                P[j] = make_float4(aa, cc, 1.0f - cc, 0.0f);
+                if (fabsf(cc) < tiny && cc != 0.0f && k <= last && l0 + l < J.nl)
+                    atomicOr(&flags[i], 1u << (k / 16 - i * (CH / 16)));
+            }
+            if (i == 0) LJ_STAMP(true, 1);
+        }
+        th_lgkm0();
+        th_barrier();
+    }
+    LJ_STAMP(true, 5);
+}
+
+template <int L>
+__device__ __forceinline__ void lj_writer(const FgsCoefJob& J, size_t fofs, int l0, int nch, int lw, int lane,
+                                          const char* lds) {
+    constexpr int CH = 1024 / L;
+    const int last = J.n - 1;
+    const float4* O = (const float4*)(lds + kLjW + kLjP);
+    const float* W = (const float*)lds;
+    for (int i = 0; i < nch + 2; i++) {
+        const int c = i - 2;
+        if (c >= 0) {
+            const float4* Oc = O + (c & 1) * 1024;
+#pragma unroll 4
+            for (int it = 0; it < 8; it++) {
+                const int j = (2 * it + lw) * 64 + lane;  // = (k - c * CH) * L + l
+                const int k = c * CH + j / L, l = j % L;
+                if (k <= last && l0 + l < J.nl) {
+                    // the solver's (den, 1/den, t); aa = lam * C[k-1] again from the weights
+                    const float4 v = Oc[j];
+                    const float aa = J.lam * (k > 0 ? W[c * 1024 + j - L] : 0.0f);
+                    const size_t o = fofs + (size_t)k * J.st + l0 + l;
+                    J.coef[o] = make_float4(aa, v.x, v.y, v.z);
+                    J.tt[o] = v.z;
+                }
+            }
+        }
+        th_barrier();
+    }
+    LJ_STAMP(lw == 0, 4);
+}
+
+template <int L>
+__device__ __forceinline__ void lj_block(const FgsCoefJob& J, size_t fofs, int jb, int wave, int lane, char* lds) {
+    constexpr int CH = 1024 / L;
+    const int l0 = jb * L, nch = (J.n + CH - 1) / CH;
+    if (wave == 0) lj_solver<L>(J.n, nch, lane, lds);
+    else if (wave == 1) lj_prep<L>(J, fofs, l0, nch, lane, lds);
+    else lj_writer<L>(J, fofs, l0, nch, wave - 2, lane, lds);
+}
+
+// The coefficient jobs of a launch (a.job, blocks of job.lpb lines each; blockIdx.y = frame).
+__global__ __launch_bounds__(256) void k_fgs_lrjob(FgsThArgs a) {
+    __shared__ __attribute__((aligned(16))) char lds[kLjLds];
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const size_t fofs = (size_t)blockIdx.y * a.fs;
+    int jb = blockIdx.x, j = 0;
+    while (j < a.njobs && jb >= a.job[j].blocks) jb -= a.job[j++].blocks;
+    if (j >= a.njobs) return;  // uniform over the workgroup
+    const FgsCoefJob& J = a.job[j];
+    LJ_STAMP(wave == 0, 0);
+    switch (J.lpb) {
+        case 16: lj_block<16>(J, fofs, jb, wave, lane, lds); break;
+        case 8: lj_block<8>(J, fofs, jb, wave, lane, lds); break;
+        default: lj_block<4>(J, fofs, jb, wave, lane, lds); break;
+    }
 }
 
 // R0 (and R1) row-major [h][w] -> the first row pass's input: transposed [w][hp] (hp = h rounded
@@ -1642,6 +1886,29 @@ static bool launch_fgs_lr(FgsThArgs a, bool two, int F, hipStream_t st) {
     return false;
 }
 
+// One k_fgs_lrjob launch for the jobs of c when every job's lines fit in LDS (n <= 6 * 1024 / L
+// for L of 16, 8, 4 lines a workgroup: the largest that fits, per job); false: take k_fgs_th.
+static bool launch_fgs_lrjob(FgsThArgs c, int F, hipStream_t st) {
+    static const bool off = getenv("SDR_FGS_LRJOB") && atoi(getenv("SDR_FGS_LRJOB")) == 0;  // A/B knob
+    if (off || c.njobs <= 0) return false;
+    int blocks = 0;
+    for (int j = 0; j < c.njobs; j++) {
+        FgsCoefJob& J = c.job[j];
+        J.lpb = 0;
+        for (int L : {16, 8, 4})  // (2 lines: the weights' 8-byte rows are not whole DMA pieces)
+            if (J.n <= kLrChunks * 1024 / L) {
+                J.lpb = L;
+                break;
+            }
+        if (!J.lpb) return false;
+        J.blocks = (J.nl + J.lpb - 1) / J.lpb;
+        blocks += J.blocks;
+    }
+    c.main_blocks = 0;
+    hipLaunchKernelGGL(k_fgs_lrjob, dim3(blocks, F), dim3(256), 0, st, c);
+    return true;
+}
+
 // k_fgs_pcr instance for G*n samples per block: one equation per thread up to 1024 samples
 // (T = the samples rounded up to whole waves), 2 or 4 per thread of 1024 beyond
 template <bool TWO, bool FIN = false>
@@ -1758,7 +2025,7 @@ static int launch_fgs(const uint8_t* guide, size_t gstride, size_t gfstride, con
                 j.st = q.st;
             }
             KScope kt(timer, SDR_KERNEL_FGS_COEF);
-            launch_fgs_th(c, false, two, F, st);
+            if (!launch_fgs_lrjob(c, F, st)) launch_fgs_th(c, false, two, F, st);
         }
         for (int p = 0; p < npass; p++) {
             KScope kt(timer, SDR_KERNEL_FGS);
@@ -2135,6 +2402,9 @@ int sdr_th_blocks(unsigned long long* host) {
 }
 int sdr_lr_blocks(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_lr_blk), 16 * 512 * 8 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+int sdr_lj_blocks(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_lj_blk), 512 * 8 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 int sdr_th_counts(unsigned int* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(sdr::g_th_counts), 16, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;

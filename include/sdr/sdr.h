@@ -161,7 +161,8 @@ int sdr_disp16_reproject_device(const int16_t* d_disp, int width, int height, si
 /* cv::filterSpeckles(img, newVal, maxSpeckleSize, maxDiff) on dense int16 frames [nframes][H][W],
  * in place, asynchronous on `stream`.  This is the post-filter StereoSGBM::compute applies with
  * newVal = (minDisparity-1)*16, maxDiff = 16*speckleRange; scratch is
- * stream-ordered (hipMallocAsync). */
+ * stream-ordered, from a device memory pool the library keeps for the process (freed blocks stay
+ * mapped for the next call). */
 int sdr_filter_speckles_device(int16_t* d_img, int width, int height, int nframes, int newVal,
                                int maxSpeckleSize, int maxDiff, void* stream);
 /* disp.convertTo(f, CV_32F, 1/16) on device. */
@@ -240,7 +241,8 @@ int sdr_wls_filter(sdr_wls* h, const int16_t* disp_left, const int16_t* disp_rig
 /* cv::ximgproc::fastGlobalSmootherFilter(guide, src, dst, lambda, sigma, attenuation, iters) on
  * nimg float images [nimg][h][w] sharing one 8-bit guide, in place, async on `stream`; solver
  * SDR_FGS_PCR or SDR_FGS_THOMAS.  SDR_FGS_THOMAS needs every pass's lambda * attenuation^k in
- * [0, 2^100] and allocates (stream-ordered, per call) 4 * (6 + 10 * num_iter) bytes a sample of
+ * [0, 2^100] and allocates (stream-ordered per call, from the library's device memory pool)
+ * 4 * (6 + 10 * num_iter) bytes a sample of
  * w x h rounded up to 4 each way: the coefficients of its 2 * num_iter passes (20 B a sample each)
  * and the pass layouts. */
 int sdr_fgs_filter_device(const uint8_t* d_guide, size_t guide_stride, int width, int height,
@@ -326,7 +328,9 @@ int sdr_xyz_to_cloud_device(const float* d_xyz, const uint8_t* d_bgr, size_t bgr
 /* pcl::VoxelGrid<PointXYZRGB> with leaf (lx, ly, lz) (pcd_write.cpp:122-130) on n device points
  * -> d_out (capacity n) and *out_count.  PCL's int32-overflow case (leaf too small for the extent,
  * the reference's 5 mm leaf on millimetre clouds) copies the input through and sets *passthrough.
- * Synchronous on `stream` (the count is a host value). */
+ * Synchronous on `stream` (the count is a host value).  Scratch: ~44 B a point plus the sort's
+ * histograms, from a grow-only device arena a call leases and returns idle (one arena per call in
+ * flight at once, kept for the process). */
 int sdr_voxel_grid_device(const void* d_points, int n, float lx, float ly, float lz, void* d_out,
                           int* out_count, int* passthrough, void* stream);
 /* pcl::io::savePCDFileBinary (pcd_write.cpp:141): header + width*height records (host memory).

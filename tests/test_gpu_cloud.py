@@ -53,6 +53,51 @@ def test_voxel_bit_exact(oracle, leaf, n):
     assert np.array_equal(u32(got.points), u32(ref))
 
 
+def test_voxel_arena_threads_and_sizes(oracle):
+    """The voxel grid's leased scratch arenas (sdr_cloud.hip, ArenaLease): calls of growing and
+    shrinking sizes reuse and grow one arena, and two threads on two streams lease one each at
+    once; every result bit-exact with the oracle."""
+    import threading
+
+    cases = []
+    for n, leaf in ((3000, 0.05), (150000, 0.5), (500, 0.05), (60000, 0.2)):
+        rng = np.random.default_rng(n)
+        pts = np.empty((n, 4), np.float32)
+        pts[:, :3] = rng.normal(0, 3, (n, 3))
+        pts[rng.random(n) < 0.1, :3] = np.nan
+        pts.view(np.uint32)[:, 3] = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        ref, passthrough = oracle.voxel_grid(pts, leaf)
+        cases.append((pts, leaf, ref, passthrough))
+    dev = torch.device("cuda", 0)
+
+    def run(order, out, stream, errors):
+        try:
+            with torch.cuda.stream(stream):
+                for i in order:
+                    pts, leaf, _, _ = cases[i]
+                    vg = VoxelGrid()
+                    vg.setLeafSize(leaf, leaf, leaf)
+                    got = vg.filter(sdr.cloud.PointCloud(torch.from_numpy(pts).to(dev), len(pts), 1))
+                    out.append((i, got.points.cpu().numpy(), vg.passthrough))
+        except Exception as e:  # noqa: BLE001 -- re-raised on the main thread
+            errors.append(e)
+
+    errors, seq = [], []
+    run([0, 1, 2, 3, 1, 0], seq, torch.cuda.current_stream(dev), errors)
+    outs = [[], []]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    threads = [threading.Thread(target=run, args=([0, 1, 2, 3] * 3, outs[k], streams[k], errors)) for k in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert len(seq) == 6 and len(outs[0]) == len(outs[1]) == 12
+    for i, got, passthrough in seq + outs[0] + outs[1]:
+        assert passthrough == cases[i][3]
+        assert np.array_equal(u32(got), u32(cases[i][2])), i
+
+
 def test_voxel_passthrough_and_empty(oracle):
     rng = np.random.default_rng(3)
     xyz = rng.uniform(-500, 500, (60, 80, 3)).astype(np.float32)

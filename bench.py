@@ -418,8 +418,24 @@ def main():
         def run(j, k, slot, ingest_events=None):
             if kind == "live":
                 return pipes[k].enqueue(sbs[j:j + batch], streams[k], ingest_events=ingest_events)
-            return pipes[k].enqueue(sbs[j:j + batch], streams[k])
+            if ns == 1:
+                return pipes[k].enqueue(sbs[j:j + batch], streams[k])
+            d = pipes[k].enqueue(sbs[j:j + batch], streams[k], voxel=False)
+            flush_voxel()
+            pending["k"] = k
+            return d
     m = ms[0]
+    # the cloud pipeline's voxel grids synchronise their stream (the counts are host values): with
+    # several streams, a step's voxel stage runs after the NEXT step's frames are enqueued on the
+    # next stream, so the GPU has that work while the host waits (every frame's voxel grid still
+    # runs, inside the timed region: flush_voxel after the loop)
+    pending = {"k": None}
+
+    def flush_voxel():
+        if pending["k"] is not None:
+            pipes[pending["k"]].voxel(streams[pending["k"]])
+            pending["k"] = None
+
     # the gather to rank 0, batched per stream: the frames a stream computes land
     # in a set of G slots (the compute writes MODE_SGBM's disparity straight into its slot), and one
     # collective per G of that stream's steps gathers the set from every rank, issued on that same
@@ -491,6 +507,7 @@ def main():
 
     for i in range(a.warmup):
         step(i, last=last_of(i, a.warmup))
+    flush_voxel()
     drain()
     if dist_on:
         check_ranks(failure["code"])
@@ -504,6 +521,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(a.warmup + i, last=last_of(a.warmup + i, a.warmup + a.steps))
+    flush_voxel()  # the last step's voxel grids, inside the timed region
     host_el = time.perf_counter() - t0  # the host's enqueue time (the GPU may still be running)
     drain()
     torch.cuda.synchronize()

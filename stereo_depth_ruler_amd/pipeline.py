@@ -127,7 +127,9 @@ class CloudEmit:
 
     def enqueue(self, sbs, stream, voxel=True):
         """sbs: uint8 (batch, H, 2W, 3) on the device.  The voxel grid returns host counts, so that
-        stage synchronises `stream` once per frame."""
+        stage synchronises `stream` once per frame; voxel=False leaves it to voxel(), which a
+        caller running several pipelines can call after enqueueing the next one's frames, so the
+        GPU has work queued while the host waits."""
         s = _vp(stream.cuda_stream)
         L = lib()
         W, H, F = self.W, self.H, self.batch
@@ -143,14 +145,22 @@ class CloudEmit:
         # convertCVMatToPCL(pointCloud_CV, left)  (:119)
         check(L.sdr_xyz_to_cloud_device(self.xyz.data_ptr(), sbs.data_ptr(), row, row * H, W, H, F,
                                         self.points.data_ptr(), s))
-        if voxel:  # VoxelGrid 5 mm  (:122-130)
-            cnt, pt = ctypes.c_int(), ctypes.c_int()
-            for f in range(F):
-                check(L.sdr_voxel_grid_device(self.points[f].data_ptr(), W * H, self.leaf, self.leaf,
-                                              self.leaf, self.filtered[f].data_ptr(), ctypes.byref(cnt),
-                                              ctypes.byref(pt), s))
-                self.counts[f], self.passthrough[f] = cnt.value, bool(pt.value)
+        if voxel:
+            self.voxel(stream)
         return self.disp
+
+    def voxel(self, stream):
+        """VoxelGrid 5 mm (:122-130) of the frames the last enqueue left in `points`, on the stream
+        that enqueued them (synchronous: the counts are host values)."""
+        s = _vp(stream.cuda_stream)
+        L = lib()
+        W, H = self.W, self.H
+        cnt, pt = ctypes.c_int(), ctypes.c_int()
+        for f in range(self.batch):
+            check(L.sdr_voxel_grid_device(self.points[f].data_ptr(), W * H, self.leaf, self.leaf,
+                                          self.leaf, self.filtered[f].data_ptr(), ctypes.byref(cnt),
+                                          ctypes.byref(pt), s))
+            self.counts[f], self.passthrough[f] = cnt.value, bool(pt.value)
 
     def close(self):
         self.m.close()

@@ -111,6 +111,42 @@ def test_voxel_passthrough_and_empty(oracle):
     assert empty.points.shape == (0, 4)
 
 
+@pytest.mark.parametrize("leaf", [0.005, 2.0])
+def test_cloud_emit_voxel_stage_behind(leaf):
+    """bench.py's C5 loop with several streams: each CloudEmit's frames enqueued with voxel=False
+    on its own stream, and its voxel stage (CloudEmit.voxel) run only after the other stream's
+    frames are queued -- the same counts, passthrough flags and filtered points as
+    enqueue(voxel=True) on one stream."""
+    from stereo_depth_ruler_amd.pipeline import CloudEmit
+
+    H, W, F = 120, 200, 2
+    dev = torch.device("cuda", 0)
+    sbs = torch.from_numpy(np.stack([S.sbs_bgr_color_frame(H, W, 64, seed=900 + i) for i in range(2 * F)])).to(dev)
+    args = (0, 64, 5, 600, 2400, 1, 63, 12, 100, 2, sdr.MODE_SGBM_3WAY)
+
+    def result(p):
+        torch.cuda.synchronize(dev)
+        return [(p.counts[f], p.passthrough[f], p.filtered[f, :p.counts[f]].cpu().numpy()) for f in range(F)]
+
+    one = CloudEmit(W, H, args, F, S.REFERENCE_Q, leaf=leaf)
+    want = []
+    for b in range(2):
+        one.enqueue(sbs[b * F:(b + 1) * F], torch.cuda.current_stream(dev))
+        want.append(result(one))
+    pipes = [CloudEmit(W, H, args, F, S.REFERENCE_Q, leaf=leaf) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    for b in range(2):
+        pipes[b].enqueue(sbs[b * F:(b + 1) * F], streams[b], voxel=False)
+    for b in range(2):
+        pipes[b].voxel(streams[b])
+    for b in range(2):
+        for (n0, p0, a0), (n1, p1, a1) in zip(want[b], result(pipes[b])):
+            assert (n0, p0) == (n1, p1)
+            assert np.array_equal(u32(a0), u32(a1))
+    for p in [one] + pipes:
+        p.close()
+
+
 @pytest.mark.parametrize("H,W,seed", [(240, 400, 41), (720, 1280, 100)])
 def test_pcd_write_pipeline(oracle, tmp_path, H, W, seed):
     """pcd_write.cpp:86-141 end to end on the device, checked byte for byte against the oracle.

@@ -140,6 +140,8 @@ struct SweepLds {
     uint4 xB[2][DW / 4][kSweepWaves * 64];
     uint32_t xdA[2][kSweepWaves * 64], xdB[2][kSweepWaves * 64];
     uint32_t sS[UP ? 1 : kSweepOwn][4][16 * DW + 4];
+    // the down pass's per-pixel epilogue queue: 16 rows of each own wave's pixels (wta_flush)
+    uint4 wq[UP ? 1 : kSweepOwn][UP ? 1 : 64 * SwShape<DW, false>::MO];
 };
 
 enum { kOwn = 0, kLeftHalo = 1, kRightHalo = 2 };
@@ -346,6 +348,48 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
         // lanes fall outside the resource and are dropped
         const int nin = max(0, min(W1, x0w + ncw) - max(x0w, 0));
 
+        // A.8's per-pixel epilogue (uniqueness, subpixel, the WTA disparity and the right view's
+        // key) for the queued pixels of rows (k & ~15) .. k, a pixel a lane: done in each row, a
+        // lane row's one pixel kept 60 of the wave's 64 lanes idle through ~45 instructions
+        auto wta_flush = [&](int k) __attribute__((always_inline)) {
+            if constexpr (WTA) {
+                const int kb = k & ~15, nrow = k - kb + 1;
+                const int invalid = (g.minD - 1) * 16;
+                const bool check_uniq = w.uniq > 0 || !w.uniq_simd;
+                // SIMD rule: S[d] < (short)(thresh + 1), thresh = (100*minS)/(100-u); scalar: S*(100-u) < 100*minS
+                const double inv100u = 1.0 / (double)(100 - w.uniq) * (1.0 + 0x1p-40);
+#pragma unroll
+                for (int q = 0; q < MO; q++) {
+                    const int e = q * 64 + lane;
+                    const int m = e % MO, rq = (e / MO) & 3, kk = e / (4 * MO);
+                    const int x = x0w + rq * MO + m;
+                    if (kk < nrow && x >= 0 && x < W1) {
+                        const uint4 v = sh.wq[wv - 1][e];
+                        const int minS = (int)(v.x >> 16), best = (int)(v.x & 0xffffu);
+                        const int Sm = (int)(int16_t)(v.y >> 16), Sp = (int)(int16_t)(v.y & 0xffffu);
+                        const int min2 = (int)v.z;
+                        const int y = yof(kb + kk);
+                        const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);
+                        const bool reject =
+                            check_uniq && (w.uniq_simd ? (min2 < thr16) : (min2 * (100 - w.uniq) < minS * 100));
+                        int out = invalid;
+                        // every S saturated: OpenCV's first-minimum scan keeps bestDisp = -1 (INVALID)
+                        if (!reject && minS < kMaxCost) {
+                            const int den = max(Sm + Sp - 2 * minS, 1);
+                            const int qq = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
+                            out = best * 16 + (((0 < best) & (best < D - 1)) ? qq : 0) + g.minD * 16;
+                            if (w.d2) {
+                                const int x2 = x + g.minX1 - g.minD - best;
+                                if (x2 >= 0 && x2 < g.W)
+                                    atomicMin(&w.d2[(size_t)f * w.disp_fstride + (size_t)y * g.W + x2],
+                                              ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
+                            }
+                        }
+                        w.disp_raw[(size_t)f * w.disp_fstride + (size_t)y * g.W + x + g.minX1] = (int16_t)out;
+                    }
+                }
+            }
+        };
         auto row = [&](const int k, auto sc) __attribute__((always_inline)) {
             constexpr int s = decltype(sc)::value;
             if (k > 0 && k % RS == 0) {
@@ -497,9 +541,6 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
                 if (!idle) {
                     // A.8 on S = sat(E + W + up + S + SE + SW) of each own slot
                     const uint32_t(&e)[EM][3][DW] = er[s % ER];
-                    const int y = yof(k);
-                    const int invalid = (g.minD - 1) * 16;
-                    const bool check_uniq = w.uniq > 0 || !w.uniq_simd;
 #pragma unroll
                     for (int m = 0; m < M; m++) {
                         uint32_t St[DW];
@@ -541,29 +582,13 @@ __device__ __forceinline__ void sweep_wave(const Geometry& g, const SweepArgs& a
                         m2 = pk_min(m2, funnel16(m2, m2));
                         m2 = row16_min_u32(m2);
                         const int min2 = (int)(m2 & 0x7fff);
-                        // SIMD rule: S[d] < (short)(thresh + 1), thresh = (100*minS)/(100-u); scalar: S*(100-u) < 100*minS
-                        const double inv100u = 1.0 / (double)(100 - w.uniq) * (1.0 + 0x1p-40);
-                        const int thr16 = (int)(short)((int)((double)(100 * minS) * inv100u) + 1);
-                        const bool reject =
-                            check_uniq && (w.uniq_simd ? (min2 < thr16) : (min2 * (100 - w.uniq) < minS * 100));
-                        const int x = col(m);
-                        if (gl == 0 && x >= 0 && x < W1) {
-                            int out = invalid;
-                            // every S saturated: OpenCV's first-minimum scan keeps bestDisp = -1 (INVALID)
-                            if (!reject && minS < kMaxCost) {
-                                const int den = max(Sm + Sp - 2 * minS, 1);
-                                const int qq = div_trunc_small((Sm - Sp) * 16 + den, 2 * den);
-                                out = best * 16 + (((0 < best) & (best < D - 1)) ? qq : 0) + g.minD * 16;
-                                if (w.d2) {
-                                    const int x2 = x + g.minX1 - g.minD - best;
-                                    if (x2 >= 0 && x2 < g.W)
-                                        atomicMin(&w.d2[(size_t)f * w.disp_fstride + (size_t)y * g.W + x2],
-                                                  ((uint32_t)minS << 16) | (uint32_t)(0xffff - x));
-                                }
-                            }
-                            w.disp_raw[(size_t)f * w.disp_fstride + (size_t)y * g.W + x + g.minX1] = (int16_t)out;
-                        }
+                        // the pixel's epilogue waits in the queue (wta_flush)
+                        if (gl == 0)
+                            sh.wq[wv - 1][((k & 15) * 4 + r) * MO + m] =
+                                make_uint4(((uint32_t)minS << 16) | (uint32_t)best,
+                                           ((uint32_t)(uint16_t)Sm << 16) | (uint32_t)(uint16_t)Sp, (uint32_t)min2, 0u);
                     }
+                    if ((k & 15) == 15 || k == H - 1) wta_flush(k);
                 }
             }
             __syncthreads();

@@ -17,6 +17,12 @@ def pytest_configure(config):
         _lib.use_library(eng)
 
 
+def hyp_examples(n: int) -> int:
+    """A hypothesis test's example count: n, times SDR_HYP_SCALE for a wider survey on the box
+    (the round's logs: profiles/r6_parity_survey/)."""
+    return max(1, int(n * float(os.environ.get("SDR_HYP_SCALE", "1"))))
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as O

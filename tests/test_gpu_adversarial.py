@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 hypothesis = pytest.importorskip("hypothesis")
 from hypothesis import HealthCheck, given, settings  # noqa: E402
+from conftest import hyp_examples  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
 import stereo_depth_ruler_amd as sdr  # noqa: E402
@@ -62,7 +63,7 @@ def sgbm_cases(draw):
                 seed=draw(st.integers(0, 10**6)))
 
 
-@settings(max_examples=80, deadline=None, derandomize=True, database=None,
+@settings(max_examples=hyp_examples(80), deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(case=sgbm_cases())
 def test_hypothesis_bit_exact(oracle, case):
@@ -115,7 +116,7 @@ def wide_block_cases(draw):
                 seed=draw(st.integers(0, 10**6)))
 
 
-@settings(max_examples=30, deadline=None, derandomize=True, database=None,
+@settings(max_examples=hyp_examples(30), deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(case=wide_block_cases())
 def test_wide_blocks_bit_exact(oracle, case):

@@ -573,9 +573,11 @@ def test_two_chain_paths_randomized(oracle):
     3WAY column chains, D <= 128), adversarial pairs included (int16 extremes)."""
     pytest.importorskip("hypothesis")
     from hypothesis import HealthCheck, given, settings
+
+    from conftest import hyp_examples
     from hypothesis import strategies as st
 
-    @settings(max_examples=6, deadline=None, derandomize=True, database=None,
+    @settings(max_examples=hyp_examples(6), deadline=None, derandomize=True, database=None,
               suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
     @given(D=st.integers(1, 8).map(lambda k: 16 * k), H=st.integers(520, 640), W1=st.integers(520, 760),
                mode=st.sampled_from([2, 3]), bs=st.sampled_from([3, 5, 7]), P1=st.integers(1, 600),

@@ -207,6 +207,7 @@ def test_two_handles_two_streams_concurrent_sweeps(oracle):
 
 hypothesis = pytest.importorskip("hypothesis")
 from hypothesis import HealthCheck, given, settings  # noqa: E402
+from conftest import hyp_examples  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
 
@@ -222,7 +223,7 @@ def sweep_cases(draw):
                 ws=draw(st.sampled_from([0, 0, 20])), seed=draw(st.integers(0, 10**6)))
 
 
-@settings(max_examples=12, deadline=None, derandomize=True, database=None,
+@settings(max_examples=hyp_examples(12), deadline=None, derandomize=True, database=None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 @given(case=sweep_cases())
 def test_hh_sweep_hypothesis_bit_exact(oracle, case):

@@ -297,11 +297,13 @@ def test_default_solver_hypothesis(oracle):
     solver's distance from it on the same inputs, recorded (it exceeds 1 level on some cases:
     that is why the default is ximgproc's order)."""
     from hypothesis import HealthCheck, given, settings
+
+    from conftest import hyp_examples
     from hypothesis import strategies as st
 
     worst = []
 
-    @settings(max_examples=24, deadline=None, derandomize=True,
+    @settings(max_examples=hyp_examples(24), deadline=None, derandomize=True,
               suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
     @given(shape=st.sampled_from([(40, 61), (97, 130), (8, 3840), (6, 4096), (3840, 3), (4096, 2), (160, 560),
                                   (33, 700)]),

@@ -1874,8 +1874,14 @@ static bool launch_fgs_lr(FgsThArgs a, bool two, int F, hipStream_t st) {
 #else
     a.dbg = -1;
 #endif
+    // at most 8 lines a workgroup by default (profiles/r6_fgs_lr_maxl.txt, C4): the 360-sample
+    // column passes on 16 lines ran ~15 % slower a sample than the row passes on 8 (the four rows'
+    // reads of 16 distinct lines conflict in LDS); capped at 8, one stream 0.4195 -> 0.413 ms with
+    // 6 frames in flight unchanged within noise; at 4, one stream 0.4123 ms but 6 frames in flight
+    // 4128 -> 3948 fps (a workgroup of ~147 KiB LDS per CU, 4x as many)
+    static const int maxl = getenv("SDR_FGS_LR_MAXL") ? atoi(getenv("SDR_FGS_LR_MAXL")) : 8;  // A/B knob
     for (int L : {16, 8, 4, 2}) {
-        if (a.n > kLrChunks * 1024 / L) continue;
+        if (L > maxl || a.n > kLrChunks * 1024 / L) continue;
         const dim3 grid((a.nl + L - 1) / L, F);
         if (L == 16) hipLaunchKernelGGL(k_fgs_lr<16>, grid, dim3(256), 0, st, a);
         else if (L == 8) hipLaunchKernelGGL(k_fgs_lr<8>, grid, dim3(256), 0, st, a);

@@ -712,8 +712,8 @@ def main():
         return {
             "bound": "latency",
             "kernel": "k_fgs_lr (sequential FGS pass, SDR_FGS_THOMAS: the lines resident in LDS, one solver "
-                      "wave per right-hand side, 4 samples x up to 16 lines a lane-instruction, two DMA "
-                      "loader / writer waves beside them)",
+                      "wave per right-hand side, 4 samples x up to 8 lines a lane-instruction (SDR_FGS_LR_MAXL), two "
+                      "DMA loader / writer waves beside them)",
             "achieved": round(samples / (avg_us * 1e-6) / 1e9, 3),
             "peak": round(samples / (floor_us * 1e-6) / 1e9, 3),
             "unit": "G line-samples/s",
